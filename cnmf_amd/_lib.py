@@ -1,0 +1,91 @@
+"""ctypes binding of libcnmf_hip.so (C ABI declared in include/cnmf_hip.h).
+
+The library is loaded AFTER `import torch`, so the HIP runtime torch already mapped
+(libamdhip64.so.7 in torch/lib) is the one the library binds to: one runtime, one set of streams
+per process ("Two HIP runtimes").  There is no CPU fallback: if the library is
+missing or fails to load, every entry point raises `HipLibraryError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+__all__ = ["HipLibraryError", "load", "lib_path", "header_path", "declared_symbols", "check",
+           "F32", "F64", "BF16", "PASS_UPDATE_W", "PASS_ACCUMULATE", "PASS_LOSS"]
+
+F32, F64, BF16 = 0, 1, 2
+PASS_UPDATE_W, PASS_ACCUMULATE, PASS_LOSS = 1, 2, 4
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class HipLibraryError(RuntimeError):
+    """The HIP extension is missing, failed to load, or a call returned an error status."""
+
+
+def lib_path() -> str:
+    return os.environ.get("CNMF_HIP_LIB", os.path.join(_HERE, "libcnmf_hip.so"))
+
+
+def header_path() -> str:
+    return os.path.join(os.path.dirname(_HERE), "include", "cnmf_hip.h")
+
+
+def declared_symbols() -> list[str]:
+    """Every function the public header declares (the ABI test checks the .so exports them)."""
+    with open(header_path()) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\**\s+\**(cnmf_[a-z_0-9]+)\(", text, re.M)))
+
+
+_vp, _i32, _i64, _f64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+
+_SIGS = {
+    "cnmf_abi_version": (_i32, []),
+    "cnmf_last_error": (ctypes.c_char_p, []),
+    "cnmf_padded_k": (_i32, [_i32]),
+    "cnmf_pass_blocks": (_i64, [_i64, _i32, _i32, _i32]),
+    "cnmf_stage_doubles": (_i64, [_i32]),
+    "cnmf_mu_sample_pass": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f64, _f64,
+                                   _i32, _vp]),
+    "cnmf_reduce_partials": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
+    "cnmf_basis_update": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _f64, _f64, _i32, _vp, _vp]),
+    "cnmf_reduce_update": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f64,
+                                  _f64, _vp, _vp]),
+    "cnmf_mu_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                  _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp]),
+}
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises HipLibraryError when unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    import torch  # noqa: F401  — map torch's HIP runtime first (see module docstring)
+
+    path = lib_path()
+    if not os.path.exists(path):
+        raise HipLibraryError(
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `python -m cnmf_amd.build` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:
+        raise HipLibraryError(f"failed to load {path}: {e}") from e
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(status: int, what: str = "") -> int:
+    """Raise HipLibraryError for a negative status, with the library's thread-local message."""
+    if status < 0:
+        msg = load().cnmf_last_error().decode(errors="replace")
+        raise HipLibraryError(f"{what or 'cnmf call'} failed ({status}): {msg}")
+    return status

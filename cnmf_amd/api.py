@@ -1,0 +1,325 @@
+"""The caller-facing boundary: sklearn-shaped `factorise` / `fit` / `non_negative_factorization`
+and the `NMF` estimator, with the argument meaning, defaults and error behaviour of
+scikit-learn 1.7.2's Frobenius MU path (SK = sklearn/decomposition/_nmf.py):
+
+  non_negative_factorization   SK:905-1131   -> factorise (aliases fit, non_negative_factorization)
+  NMF.fit_transform/transform  SK:1600-1763  -> NMF
+  _check_init / _check_w_h      SK:68-82, SK:1194-1252
+  _compute_regularization       SK:1254-1265
+  _initialize_nmf ('random')    SK:303-314   (nndsvd / nndsvda / nndsvdar: cnmf_amd.init)
+
+Differences, all deliberate: the only solver is 'mu' (the default here; sklearn's default 'cd'
+raises), only beta_loss='frobenius' is accepted, sparse X is not, and n_components ≤ 16.  NumPy
+inputs are copied to the GPU and results come back as NumPy arrays of X's dtype; torch tensors on a
+HIP device stay there (fp32, fp64 or bf16 X; bf16 computes in fp32 and returns fp32 W/H).
+There is no CPU fallback: without the HIP library every call raises HipLibraryError.
+"""
+from __future__ import annotations
+
+import numbers
+import warnings
+
+import numpy as np
+
+from . import init as _init
+from .synthetic import random_init
+
+__all__ = ["factorise", "fit", "non_negative_factorization", "NMF", "ConvergenceWarning"]
+
+try:  # keep sklearn's warning class when it is importable (drop-in); never required
+    from sklearn.exceptions import ConvergenceWarning  # type: ignore
+except Exception:  # pragma: no cover
+    class ConvergenceWarning(UserWarning):
+        """Custom warning to capture convergence problems (sklearn.exceptions.ConvergenceWarning)."""
+
+_INITS = {"random", "nndsvd", "nndsvda", "nndsvdar", "custom", None}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _is_torch(a) -> bool:
+    try:
+        import torch
+    except Exception:  # pragma: no cover
+        return False
+    return isinstance(a, torch.Tensor)
+
+
+# ------------------------------------------------------------------------------------------------
+# validation (messages follow sklearn's)
+# ------------------------------------------------------------------------------------------------
+def _check_X(X):
+    if _is_torch(X):
+        torch = _torch()
+        if X.dim() != 2:
+            raise ValueError(f"Expected 2D array, got {X.dim()}D array instead")
+        if X.dtype not in (torch.float32, torch.float64, torch.bfloat16):
+            X = X.to(torch.float64)
+        if not bool(torch.isfinite(X).all()):
+            raise ValueError("Input X contains NaN or infinity.")
+        return X
+    X = np.asarray(X)
+    if X.ndim != 2:
+        raise ValueError(f"Expected 2D array, got {X.ndim}D array instead")
+    if X.dtype not in (np.float32, np.float64):
+        X = X.astype(np.float64)
+    if X.shape[0] < 1 or X.shape[1] < 1:
+        raise ValueError(f"Found array with shape {X.shape}; a minimum of 1 is required.")
+    if not np.isfinite(X).all():
+        raise ValueError("Input X contains NaN or infinity.")
+    return np.ascontiguousarray(X)
+
+
+def _min(a):
+    return float(a.min()) if not _is_torch(a) else float(a.min().item())
+
+
+def _max(a):
+    return float(a.max()) if not _is_torch(a) else float(a.max().item())
+
+
+def _check_non_negative(A, whom):
+    if _min(A) < 0:
+        raise ValueError(f"Negative values in data passed to {whom}.")
+
+
+def _check_init(A, shape, whom):
+    """SK:68-82."""
+    if A is None:
+        raise ValueError(f"{whom} must be provided when init='custom'")
+    A = A if _is_torch(A) else np.asarray(A)
+    if A.ndim != 2:
+        raise ValueError(f"Expected 2D array, got {A.ndim}D array instead")
+    if shape[0] != "auto" and A.shape[0] != shape[0]:
+        raise ValueError(f"Array with wrong first dimension passed to {whom}. Expected {shape[0]}, "
+                         f"but got {A.shape[0]}.")
+    if shape[1] != "auto" and A.shape[1] != shape[1]:
+        raise ValueError(f"Array with wrong second dimension passed to {whom}. Expected {shape[1]}, "
+                         f"but got {A.shape[1]}.")
+    _check_non_negative(A, whom)
+    if _max(A) == 0:
+        raise ValueError(f"Array passed to {whom} is full of zeros.")
+    return A
+
+
+def _dtype_name(a):
+    return str(a.dtype).replace("torch.", "")
+
+
+def _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H,
+                     l1_ratio):
+    if not (n_components is None or n_components == "auto" or
+            (isinstance(n_components, numbers.Integral) and not isinstance(n_components, bool)
+             and n_components >= 1)):
+        raise ValueError(f"The 'n_components' parameter must be an int in the range [1, inf), "
+                         f"None or 'auto'. Got {n_components!r} instead.")
+    if init not in _INITS:
+        raise ValueError(f"The 'init' parameter must be a str among {{'custom', 'nndsvd', "
+                         f"'nndsvda', 'nndsvdar', 'random'}} or None. Got {init!r} instead.")
+    if solver != "mu":
+        raise ValueError(f"solver={solver!r} is not available: this build implements the "
+                         "multiplicative-update solver ('mu') only.")
+    if beta_loss not in ("frobenius", 2, 2.0):
+        raise ValueError(f"beta_loss={beta_loss!r} is not available: only 'frobenius' (2) is "
+                         "implemented on the MI355X path.")
+    if not isinstance(tol, numbers.Real) or tol < 0:
+        raise ValueError(f"The 'tol' parameter must be a float in the range [0, inf). Got {tol!r} instead.")
+    if not isinstance(max_iter, numbers.Integral) or isinstance(max_iter, bool) or max_iter < 1:
+        raise ValueError(f"The 'max_iter' parameter must be an int in the range [1, inf). "
+                         f"Got {max_iter!r} instead.")
+    if not isinstance(alpha_W, numbers.Real) or alpha_W < 0:
+        raise ValueError(f"The 'alpha_W' parameter must be a float in the range [0, inf). Got {alpha_W!r} instead.")
+    if not (alpha_H == "same" or (isinstance(alpha_H, numbers.Real) and alpha_H >= 0)):
+        raise ValueError(f"The 'alpha_H' parameter must be a float in the range [0, inf) or a str "
+                         f"among {{'same'}}. Got {alpha_H!r} instead.")
+    if not isinstance(l1_ratio, numbers.Real) or not 0 <= l1_ratio <= 1:
+        raise ValueError(f"The 'l1_ratio' parameter must be a float in the range [0, 1]. Got {l1_ratio!r} instead.")
+
+
+def _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio):
+    """SK:1254-1265."""
+    alpha_H = alpha_W if alpha_H == "same" else alpha_H
+    return (n_features * alpha_W * l1_ratio, n_samples * alpha_H * l1_ratio,
+            n_features * alpha_W * (1.0 - l1_ratio), n_samples * alpha_H * (1.0 - l1_ratio))
+
+
+# ------------------------------------------------------------------------------------------------
+# the core fit
+# ------------------------------------------------------------------------------------------------
+def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
+                   l1_ratio, random_state, verbose, device, group=None, return_plan=False):
+    """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
+    torch = _torch()
+    from .solver import MUPlan, run_mu
+
+    X = _check_X(X)
+    as_torch = _is_torch(X)
+    n_samples, n_features = X.shape
+    k = n_components
+    if k is None:
+        k = n_features
+    if k == "auto":
+        if init == "custom" or not update_H:
+            k = "auto"
+        else:
+            k = n_features
+
+    # _check_w_h (SK:1194-1252)
+    if init == "custom" and update_H:
+        H = _check_init(H, (k, n_features), "NMF (input H)")
+        W = _check_init(W, (n_samples, k), "NMF (input W)")
+        if k == "auto":
+            k = H.shape[0]
+        if H.dtype != X.dtype or W.dtype != X.dtype:
+            if not (as_torch and X.dtype == torch.bfloat16):
+                raise TypeError("H and W should have the same dtype as X. Got H.dtype = {} and "
+                                "W.dtype = {}.".format(_dtype_name(H), _dtype_name(W)))
+    elif not update_H:
+        if W is not None:
+            warnings.warn("When update_H=False, the provided initial W is not used.", RuntimeWarning)
+        H = _check_init(H, (k, n_features), "NMF (input H)")
+        if k == "auto":
+            k = H.shape[0]
+        if H.dtype != X.dtype and not (as_torch and X.dtype == torch.bfloat16):
+            raise TypeError("H should have the same dtype as X. Got H.dtype = {}.".format(_dtype_name(H)))
+        W = None  # filled with sqrt(X.mean()/k) below (SK:1228-1232)
+    else:
+        if W is not None or H is not None:
+            warnings.warn("When init!='custom', provided W or H are ignored. Set  init='custom' to "
+                          "use them as initialization.", RuntimeWarning)
+        if k == "auto":
+            k = n_features
+        Xh = X if not as_torch else X.detach().to("cpu", torch.float32 if X.dtype == torch.bfloat16 else X.dtype).numpy()
+        W, H = _init.initialize_nmf(Xh, k, init=init, random_state=random_state)
+    k = int(k)
+    if k > 16:
+        raise ValueError(f"n_components={k} is not supported: the MI355X kernels handle 1..16.")
+
+    regs = _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio)
+    dev = torch.device(device) if device is not None else (X.device if as_torch else torch.device("cuda", torch.cuda.current_device()))
+    Xd = X if as_torch else torch.from_numpy(X)
+    Xd = Xd.to(dev, non_blocking=False).contiguous()
+    plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
+    if W is None:  # update_H=False start: sqrt(X.mean()/k) in X's dtype (SK:1228-1232)
+        if as_torch:
+            avg = float(torch.sqrt(X.double().mean() / k))
+        else:
+            avg = float(np.sqrt(X.mean() / k))
+        plan.W.fill_(avg)
+    else:
+        plan.set_W(W if _is_torch(W) else torch.from_numpy(np.ascontiguousarray(W)))
+    plan.set_H(H if _is_torch(H) else torch.from_numpy(np.ascontiguousarray(H)))
+    n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H, verbose=verbose)
+    if n_iter == max_iter and tol > 0:
+        warnings.warn("Maximum number of iterations %d reached. Increase it to improve "
+                      "convergence." % max_iter, ConvergenceWarning)
+    Wd, Hd = plan.W, plan.H()
+    if return_plan:
+        return Wd, Hd, n_iter, plan, as_torch, X
+    return _out(Wd, as_torch, X), _out(Hd, as_torch, X), n_iter
+
+
+def _out(t, as_torch, X):
+    if as_torch:
+        return t
+    return t.detach().cpu().numpy().astype(X.dtype, copy=False)
+
+
+def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
+              beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
+              l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None):
+    """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
+
+    Same signature, argument meaning, return value (W, H, n_iter) and errors as
+    `sklearn.decomposition.non_negative_factorization` (SK:905-1131), except solver defaults to
+    (and must be) 'mu'.  `device` selects the HIP device (default: current).
+    """
+    _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
+    return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
+                          l1_ratio, random_state, verbose, device)
+
+
+fit = factorise
+non_negative_factorization = factorise
+
+
+class NMF:
+    """sklearn-shaped estimator (SK:1325-1763) on the MI355X MU path.
+
+    Attributes after fit: components_, n_components_, n_iter_, reconstruction_err_,
+    n_features_in_.
+    """
+
+    def __init__(self, n_components="auto", *, init=None, solver="mu", beta_loss="frobenius",
+                 tol=1e-4, max_iter=200, random_state=None, alpha_W=0.0, alpha_H="same",
+                 l1_ratio=0.0, verbose=0, shuffle=False, device=None):
+        self.n_components = n_components
+        self.init = init
+        self.solver = solver
+        self.beta_loss = beta_loss
+        self.tol = tol
+        self.max_iter = max_iter
+        self.random_state = random_state
+        self.alpha_W = alpha_W
+        self.alpha_H = alpha_H
+        self.l1_ratio = l1_ratio
+        self.verbose = verbose
+        self.shuffle = shuffle
+        self.device = device
+
+    def get_params(self, deep=True):
+        return {k: getattr(self, k) for k in ("n_components", "init", "solver", "beta_loss", "tol",
+                                              "max_iter", "random_state", "alpha_W", "alpha_H",
+                                              "l1_ratio", "verbose", "shuffle", "device")}
+
+    def set_params(self, **params):
+        for k, v in params.items():
+            setattr(self, k, v)
+        return self
+
+    def _validate(self):
+        _validate_params(self.n_components, self.init, self.solver, self.beta_loss, self.tol,
+                         self.max_iter, self.alpha_W, self.alpha_H, self.l1_ratio)
+
+    def fit_transform(self, X, y=None, W=None, H=None):
+        """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H."""
+        self._validate()
+        Wd, Hd, n_iter, plan, as_torch, Xc = _fit_transform(
+            X, W, H, self.n_components, self.init, True, self.tol, self.max_iter, self.alpha_W,
+            self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
+            return_plan=True)
+        self.reconstruction_err_ = plan.frobenius_error()
+        self.n_components_ = int(Hd.shape[0])
+        self.components_ = _out(Hd, as_torch, Xc)
+        self.n_iter_ = n_iter
+        self.n_features_in_ = int(Xc.shape[1])
+        return _out(Wd, as_torch, Xc)
+
+    def fit(self, X, y=None, **params):
+        self.fit_transform(X, **params)
+        return self
+
+    def transform(self, X):
+        """SK:1736-1763: solve for W with components_ fixed (update_H=False)."""
+        if not hasattr(self, "components_"):
+            raise ValueError("This NMF instance is not fitted yet. Call 'fit' with appropriate "
+                             "arguments before using this estimator.")
+        X = _check_X(X)
+        _check_non_negative(X, "NMF (input X)")
+        if X.shape[1] != self.n_features_in_:
+            raise ValueError(f"X has {X.shape[1]} features, but NMF is expecting "
+                             f"{self.n_features_in_} features as input.")
+        W, _, _ = _fit_transform(X, None, self.components_, self.n_components_, self.init, False,
+                                 self.tol, self.max_iter, self.alpha_W, self.alpha_H,
+                                 self.l1_ratio, self.random_state, self.verbose, self.device)
+        return W
+
+    def inverse_transform(self, X=None, *, Xt=None):
+        """W·H back in data space (SK `_BaseNMF.inverse_transform`)."""
+        X = Xt if X is None else X
+        if _is_torch(X):
+            return X @ self.components_
+        return np.asarray(X) @ self.components_

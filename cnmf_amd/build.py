@@ -1,0 +1,47 @@
+"""Build libcnmf_hip.so in-tree with hipcc for gfx950 (no JIT cache, no torch extension machinery).
+
+    python -m cnmf_amd.build [--verbose]
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "cnmf_hip.hip")
+OUT = os.path.join(HERE, "libcnmf_hip.so")
+ARCH = os.environ.get("CNMF_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    out_m = os.path.getmtime(OUT)
+    deps = [SRC, os.path.join(ROOT, "include", "cnmf_hip.h")]
+    return any(os.path.getmtime(d) > out_m for d in deps if os.path.exists(d))
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    cmd = [hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
+           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv))

@@ -1,0 +1,862 @@
+// cnmf_hip.hip — MI355X (gfx950, CDNA4) kernels + C ABI for the Frobenius multiplicative update.
+//
+// What runs per MU iteration (sklearn naming, X[N][F] samples-major):
+//
+//   mu_pass_kernel      ONE streaming pass over X and W (the ~all-bytes kernel):
+//                       per 64-sample tile staged in LDS: num = X·Hᵀ, den = W·HHᵀ (+l1)(+l2·W),
+//                       W <- W·(num/den) written back, then the accumulators [WᵀX | WᵀW] of the
+//                       NEW W folded into per-workgroup fp64 partials.       (SK:526-631, SK:639-640)
+//   reduce_kernel       deterministic fp64 column-sum of the per-workgroup partials (fixed slice
+//                       order, ticket-elected last workgroup combines the slices) and, fused for a
+//                       single GPU, the basis update in that last workgroup.
+//   basis_update        H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) in fp64, then Ht / HHt for the next
+//                       pass.                                                 (SK:634-728)
+//
+// SK:<line> = sklearn/decomposition/_nmf.py (1.7.2), the algorithm the reference declares
+// (/root/reference/setup.py:26,30; the reference's own cnmf/__init__.py is empty).
+//
+// Design notes (MI355X-first; see DESIGN.md for the roofline numbers):
+//  * the pass is HBM-bound (≈4 flop/B): each workgroup (4 waves) streams whole 64-sample tiles of X
+//    (64·F contiguous elements) and W through 16-byte register loads issued one tile AHEAD of the
+//    compute (the next tile is in flight while the current one is reduced), then stores them
+//    verbatim to LDS; no HBM byte is read twice per iteration.
+//  * per-sample work maps lane = sample (num, update); the outer-product accumulation maps
+//    lane = feature (A phase), so the k×(F+k) accumulators live in registers for the whole
+//    launch and only ONE fp64 partial row per workgroup reaches HBM.
+//  * precision: per-tile fp32 accumulation (16 or 64 terms), fp64 running sums, fp64 cross-block
+//    reduction and fp64 basis update (H is kept in fp64 on the device) so the fp32 path tracks the
+//    fp64 CPU oracle (≤1e-5 rel. Frobenius after 500 iterations).
+//  * grid = persistent, sized from the occupancy query so that ceil(tiles/blocks) rounds are
+//    balanced; tiles are dealt round-robin so concurrently running workgroups stream neighbouring
+//    addresses.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+
+#include "cnmf_hip.h"
+
+namespace cnmf {
+
+constexpr int TS = 64;       // samples per tile
+constexpr int NT = 256;      // threads per workgroup
+constexpr int NWAVE = NT / 64;
+constexpr int PF = 8;        // 16-byte chunks per thread held in registers for the next tile
+constexpr int NSLICE = 16;   // slices of the deterministic cross-block reduction
+constexpr int RED_NT = 256;  // threads of the reduce / update workgroups
+constexpr double EPS32 = 1.1920928955078125e-07;  // np.finfo(np.float32).eps, SK:39
+
+static thread_local char g_err[512] = "";
+
+static int set_err(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return set_err(CNMF_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));        \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// element conversions: X storage type -> compute type
+// ------------------------------------------------------------------------------------------------
+struct bf16_t {
+  uint16_t bits;
+};
+
+__device__ __forceinline__ float to_c(float v) { return v; }
+__device__ __forceinline__ double to_c(double v) { return v; }
+__device__ __forceinline__ float to_c(bf16_t v) { return __uint_as_float(((uint32_t)v.bits) << 16); }
+
+template <typename TX>
+struct Compute;
+template <>
+struct Compute<float> {
+  using T = float;
+};
+template <>
+struct Compute<double> {
+  using T = double;
+};
+template <>
+struct Compute<bf16_t> {
+  using T = float;
+};
+
+__host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
+
+// LDS carve of the pass kernel (bytes); identical on host and device.
+struct PassLds {
+  size_t region0;  // X tile, later reused for the cross-wave reduction
+  size_t w;        // old-W tile, flat [ns][k]
+  size_t wn;       // new-W tile, [TS][KP]
+  size_t p;        // partial num, [NWAVE][TS][KP]
+  size_t hht;      // HHt, [KP][KP]
+  size_t total;
+};
+
+__host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc) {
+  PassLds L;
+  size_t xb = align16((size_t)TS * F * sx);
+  size_t rb = (size_t)NWAVE * 64 * KP * sizeof(double);
+  L.region0 = xb > rb ? xb : rb;
+  L.w = L.region0;
+  L.wn = L.w + align16((size_t)TS * KP * sc);
+  L.p = L.wn + align16((size_t)TS * KP * sc);
+  L.hht = L.p + align16((size_t)NWAVE * TS * KP * sc);
+  L.total = L.hht + align16((size_t)KP * KP * sc);
+  return L;
+}
+
+// Geometry of one tile's contiguous byte ranges in X and W.
+struct TileGeom {
+  const unsigned char* xsrc;
+  const unsigned char* wsrc;
+  int ns;        // valid samples
+  int nxf;       // full 16-byte chunks of X
+  int nch;       // full chunks of X + W
+  int rx;        // trailing X elements (partial chunk)
+  int rw;        // trailing W elements
+  int nwf;
+};
+
+template <typename TX, typename TC>
+__device__ __forceinline__ TileGeom tile_geom(const TX* X, const TC* W, int64_t tile, int64_t n_rows,
+                                              int F, int k) {
+  TileGeom g;
+  int64_t s0 = tile * TS;
+  int64_t rem = n_rows - s0;
+  g.ns = rem < TS ? (int)rem : TS;
+  size_t xb = (size_t)g.ns * F * sizeof(TX);
+  size_t wb = (size_t)g.ns * k * sizeof(TC);
+  g.xsrc = reinterpret_cast<const unsigned char*>(X) + (size_t)s0 * F * sizeof(TX);
+  g.wsrc = reinterpret_cast<const unsigned char*>(W) + (size_t)s0 * k * sizeof(TC);
+  g.nxf = (int)(xb >> 4);
+  g.nwf = (int)(wb >> 4);
+  g.nch = g.nxf + g.nwf;
+  g.rx = (int)((xb & 15) / sizeof(TX));
+  g.rw = (int)((wb & 15) / sizeof(TC));
+  return g;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused sample pass.
+//   TX: X storage (float / double / bf16_t), TC: compute + W type, KP: padded k (4/8/16),
+//   NPW: 64-lane feature passes held in registers per wave, SPLIT: A phase splits the tile's
+//   samples over the 4 waves (few passes) or splits the passes over the waves (wide rows).
+// ------------------------------------------------------------------------------------------------
+template <typename TX, int KP, int NPW, bool SPLIT>
+__global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
+                                                     typename Compute<TX>::T* __restrict__ W,
+                                                     const typename Compute<TX>::T* __restrict__ Ht,
+                                                     const typename Compute<TX>::T* __restrict__ HHt,
+                                                     double* __restrict__ partials, int64_t n_rows,
+                                                     int F, int k, typename Compute<TX>::T l1,
+                                                     typename Compute<TX>::T l2, int flags,
+                                                     int64_t n_tiles) {
+  using TC = typename Compute<TX>::T;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC));
+  TX* sX = reinterpret_cast<TX*>(smem);
+  TC* sW = reinterpret_cast<TC*>(smem + L.w);
+  TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
+  TC* sP = reinterpret_cast<TC*>(smem + L.p);
+  TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
+  double* sRed = reinterpret_cast<double*>(smem);
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int V = F + k;
+  const int np = (V + 63) >> 6;
+  const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+  const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
+
+  for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
+
+  double acc64[NPW][KP];
+#pragma unroll
+  for (int i = 0; i < NPW; ++i)
+#pragma unroll
+    for (int j = 0; j < KP; ++j) acc64[i][j] = 0.0;
+  double loss64 = 0.0;
+
+  uint4 pf[PF];
+  int64_t tile = blockIdx.x;
+  if (tile < n_tiles) {
+    TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      int c = t + NT * i;
+      if (c < g.nch) {
+        const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
+        pf[i] = *reinterpret_cast<const uint4*>(src);
+      }
+    }
+  }
+
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
+    const int ns = g.ns;
+    // ---- stage tile `tile` (prefetched registers + any overflow chunks + ragged tail) into LDS
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      int c = t + NT * i;
+      if (c < g.nch) {
+        unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
+        *reinterpret_cast<uint4*>(dst) = pf[i];
+      }
+    }
+    for (int c = t + NT * PF; c < g.nch; c += NT) {
+      const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
+      unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+    }
+    if (t < g.rx) {
+      int e = g.nxf * (16 / (int)sizeof(TX)) + t;
+      sX[e] = reinterpret_cast<const TX*>(g.xsrc)[e];
+    }
+    if (t >= 64 && t - 64 < g.rw) {
+      int e = g.nwf * (16 / (int)sizeof(TC)) + (t - 64);
+      sW[e] = reinterpret_cast<const TC*>(g.wsrc)[e];
+    }
+    __syncthreads();
+
+    // ---- issue the next tile's loads; they stay in flight through this tile's compute
+    {
+      const int64_t nt = tile + gridDim.x;
+      if (nt < n_tiles) {
+        TileGeom gn = tile_geom(X, W, nt, n_rows, F, k);
+#pragma unroll
+        for (int i = 0; i < PF; ++i) {
+          int c = t + NT * i;
+          if (c < gn.nch) {
+            const unsigned char* src =
+                c < gn.nxf ? gn.xsrc + 16 * (size_t)c : gn.wsrc + 16 * (size_t)(c - gn.nxf);
+            pf[i] = *reinterpret_cast<const uint4*>(src);
+          }
+        }
+      }
+    }
+
+    // ---- phase 1: lane = sample, wave = quarter of the features
+    {
+      const int q = (F + NWAVE - 1) / NWAVE;
+      const int fb = wave * q;
+      const int fe = min(F, fb + q);
+      const TX* xr = sX + (size_t)lane * F;
+      if (do_loss) {
+        TC w[KP];
+#pragma unroll
+        for (int j = 0; j < KP; ++j) w[j] = (j < k && lane < ns) ? sW[lane * k + j] : TC(0);
+        TC part = 0;
+        for (int f = fb; f < fe; ++f) {
+          const TC xv = to_c(xr[f]);
+          const TC* hr = Ht + (size_t)f * KP;
+          TC wh = 0;
+#pragma unroll
+          for (int j = 0; j < KP; ++j) wh = fma(w[j], hr[j], wh);
+          const TC r = xv - wh;
+          part = fma(r, r, part);
+        }
+        if (lane < ns) loss64 += (double)part;
+      } else {
+        TC p[KP];
+#pragma unroll
+        for (int j = 0; j < KP; ++j) p[j] = 0;
+#pragma unroll 4
+        for (int f = fb; f < fe; ++f) {
+          const TC xv = to_c(xr[f]);
+          const TC* hr = Ht + (size_t)f * KP;
+#pragma unroll
+          for (int j = 0; j < KP; ++j) p[j] = fma(xv, hr[j], p[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < KP; ++j) sP[(wave * TS + lane) * KP + j] = p[j];
+      }
+    }
+    __syncthreads();
+
+    if (do_upd) {
+      // ---- phase 2: element (s, j) = flat index e of the [TS][KP] tile; W <- W·(num/den)
+#pragma unroll
+      for (int c = 0; c < KP / 4; ++c) {
+        const int e = t + NT * c;
+        const int s = e / KP;
+        const int j = e % KP;
+        TC wn = 0;
+        if (s < ns && j < k) {
+          const TC num = sP[(0 * TS + s) * KP + j] + sP[(1 * TS + s) * KP + j] +
+                         sP[(2 * TS + s) * KP + j] + sP[(3 * TS + s) * KP + j];
+          TC den = 0;
+#pragma unroll
+          for (int m = 0; m < KP; ++m)
+            if (m < k) den = fma(sW[s * k + m], sHHt[m * KP + j], den);
+          const TC wold = sW[s * k + j];
+          if (l1 > TC(0)) den += l1;                    // SK:616-617
+          if (l2 > TC(0)) den = den + l2 * wold;        // SK:618-619
+          if (den == TC(0)) den = TC(EPS32);            // SK:620
+          const TC qv = num / den;                      // SK:622
+          wn = wold * qv;                               // SK:629
+          W[(size_t)(tile * TS + s) * k + j] = wn;
+        }
+        sWn[s * KP + j] = wn;
+      }
+      __syncthreads();
+    }
+
+    if (do_acc) {
+      // ---- phase 3: lane = virtual feature v (v < F: X column, F <= v < F+k: W_new column);
+      //      acc[j][v] += w_new[s][j] · value[s][v]   (the rows of [WᵀX | WᵀW], SK:639-640)
+      if (SPLIT) {
+        const int s_beg = wave * (TS / NWAVE);
+        const int s_end = min(ns, s_beg + TS / NWAVE);
+        TC a32[NPW][KP];
+#pragma unroll
+        for (int i = 0; i < NPW; ++i)
+#pragma unroll
+          for (int j = 0; j < KP; ++j) a32[i][j] = 0;
+        for (int s = s_beg; s < s_end; ++s) {
+          TC wv[KP];
+#pragma unroll
+          for (int j = 0; j < KP; ++j) wv[j] = sWn[s * KP + j];
+#pragma unroll
+          for (int i = 0; i < NPW; ++i) {
+            if (i < np) {
+              const int v = 64 * i + lane;
+              TC val;
+              if (64 * i + 64 <= F) {
+                val = to_c(sX[(size_t)s * F + v]);
+              } else {
+                const TC vx = to_c(sX[(size_t)s * F + min(v, F - 1)]);
+                const TC vw = sWn[s * KP + min(max(v - F, 0), KP - 1)];
+                val = v < F ? vx : (v < V ? vw : TC(0));
+              }
+#pragma unroll
+              for (int j = 0; j < KP; ++j) a32[i][j] = fma(wv[j], val, a32[i][j]);
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < NPW; ++i)
+#pragma unroll
+          for (int j = 0; j < KP; ++j) acc64[i][j] += (double)a32[i][j];
+      } else {
+#pragma unroll
+        for (int i = 0; i < NPW; ++i) {
+          const int p = wave + NWAVE * i;
+          if (p < np) {
+            const int v = 64 * p + lane;
+            const bool full = 64 * p + 64 <= F;
+            TC a32[KP];
+#pragma unroll
+            for (int j = 0; j < KP; ++j) a32[j] = 0;
+            for (int s = 0; s < ns; ++s) {
+              TC wv[KP];
+#pragma unroll
+              for (int j = 0; j < KP; ++j) wv[j] = sWn[s * KP + j];
+              TC val;
+              if (full) {
+                val = to_c(sX[(size_t)s * F + v]);
+              } else {
+                const TC vx = to_c(sX[(size_t)s * F + min(v, F - 1)]);
+                const TC vw = sWn[s * KP + min(max(v - F, 0), KP - 1)];
+                val = v < F ? vx : (v < V ? vw : TC(0));
+              }
+#pragma unroll
+              for (int j = 0; j < KP; ++j) a32[j] = fma(wv[j], val, a32[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < KP; ++j) acc64[i][j] += (double)a32[j];
+          }
+        }
+      }
+    }
+    __syncthreads();  // LDS tiles are rewritten by the next iteration
+  }
+
+  // ---- per-workgroup partial rows
+  if (do_acc) {
+    const int n_out = k * V;
+    double* prow = partials + (size_t)blockIdx.x * n_out;
+    if (SPLIT) {
+#pragma unroll
+      for (int i = 0; i < NPW; ++i) {
+        if (i < np) {
+          __syncthreads();
+#pragma unroll
+          for (int j = 0; j < KP; ++j) sRed[(wave * 64 + lane) * KP + j] = acc64[i][j];
+          __syncthreads();
+          for (int e = t; e < 64 * KP; e += NT) {
+            const int l = e & 63;
+            const int j = e >> 6;
+            const int v = 64 * i + l;
+            if (v < V && j < k) {
+              const double sum = sRed[(0 * 64 + l) * KP + j] + sRed[(1 * 64 + l) * KP + j] +
+                                 sRed[(2 * 64 + l) * KP + j] + sRed[(3 * 64 + l) * KP + j];
+              prow[j * V + v] = sum;
+            }
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NPW; ++i) {
+        const int p = wave + NWAVE * i;
+        const int v = 64 * p + lane;
+        if (p < np && v < V) {
+#pragma unroll
+          for (int j = 0; j < KP; ++j)
+            if (j < k) prow[j * V + v] = acc64[i][j];
+        }
+      }
+    }
+  }
+  if (do_loss) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) loss64 += __shfl_xor(loss64, off);
+    __syncthreads();
+    if (lane == 0) sRed[wave] = loss64;
+    __syncthreads();
+    if (t == 0) partials[blockIdx.x] = ((sRed[0] + sRed[1]) + sRed[2]) + sRed[3];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Basis update (one workgroup): the k×F epilogue, all in fp64.
+// ------------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t update_lds_doubles(int F, int k, int KP) {
+  return (size_t)k * F + (size_t)k * k + (size_t)KP * KP + RED_NT * 2;
+}
+
+template <typename TC>
+__device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HHt, int F, int k,
+                                   int KP, double l1, double l2, int do_update, double* stats,
+                                   double* lds) {
+  const int t = threadIdx.x;
+  const int V = F + k;
+  double* sH = lds;               // [k][F] new H
+  double* sB = sH + (size_t)k * F;  // [k][k] WᵀW
+  double* sHH = sB + (size_t)k * k;  // [KP][KP]
+  double* sR = sHH + (size_t)KP * KP;  // [2][RED_NT]
+
+  for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
+  __syncthreads();
+  for (int e = t; e < k * F; e += RED_NT) {
+    const int j = e / F;
+    const int f = e - j * F;
+    double h = H64[e];
+    if (do_update) {
+      const double num = AB[j * V + f];                       // (WᵀX)[j][f], SK:639
+      double den = 0.0;                                       // ((WᵀW)·H)[j][f], SK:640
+      for (int m = 0; m < k; ++m) den = fma(sB[j * k + m], H64[m * F + f], den);
+      if (l1 > 0.0) den += l1;                                // SK:702-703
+      if (l2 > 0.0) den = den + l2 * h;                       // SK:704-705
+      if (den == 0.0) den = EPS32;                            // SK:706
+      h = h * (num / den);                                    // SK:722-726
+    }
+    sH[e] = h;
+  }
+  __syncthreads();
+  for (int e = t; e < k * F; e += RED_NT) H64[e] = sH[e];
+  for (int e = t; e < F * KP; e += RED_NT) {
+    const int f = e / KP;
+    const int j = e - f * KP;
+    Ht[e] = j < k ? (TC)sH[j * F + f] : TC(0);
+  }
+  for (int e = t; e < KP * KP; e += RED_NT) {
+    const int j = e / KP;
+    const int m = e - j * KP;
+    double v = 0.0;
+    if (j < k && m < k)
+      for (int f = 0; f < F; ++f) v = fma(sH[j * F + f], sH[m * F + f], v);
+    sHH[e] = v;
+    HHt[e] = (TC)v;
+  }
+  if (stats) {
+    __syncthreads();
+    double a = 0.0, b = 0.0;
+    for (int e = t; e < k * F; e += RED_NT) a = fma(AB[(e / F) * V + (e % F)], sH[e], a);
+    for (int e = t; e < k * k; e += RED_NT) b = fma(sB[e], sHH[(e / k) * KP + (e % k)], b);
+    sR[t] = a;
+    sR[RED_NT + t] = b;
+    __syncthreads();
+    for (int s = RED_NT / 2; s > 0; s >>= 1) {
+      if (t < s) {
+        sR[t] += sR[t + s];
+        sR[RED_NT + t] += sR[RED_NT + t + s];
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      stats[0] = sR[0];
+      stats[1] = sR[RED_NT];
+    }
+  }
+}
+
+template <typename TC>
+__global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __restrict__ AB,
+                                                              double* __restrict__ H64,
+                                                              TC* __restrict__ Ht,
+                                                              TC* __restrict__ HHt, int F, int k,
+                                                              int KP, double l1, double l2,
+                                                              int do_update, double* stats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  basis_update_block<TC>(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats,
+                         reinterpret_cast<double*>(smem));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Deterministic fp64 reduction of partials[n_parts][n_out]; optional fused basis update.
+// grid = (ceil(n_out/64), NSLICE); the ticket-elected last workgroup sums the NSLICE stage rows.
+// ------------------------------------------------------------------------------------------------
+struct UpdateArgs {
+  double* H64;
+  void* Ht;
+  void* HHt;
+  int F, k, KP;
+  double l1, l2;
+  double* stats;
+  int tc_double;
+};
+
+__global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict__ partials,
+                                                        int64_t n_parts, int n_out,
+                                                        double* __restrict__ stage,
+                                                        uint32_t* __restrict__ counter,
+                                                        double* __restrict__ out, int fuse,
+                                                        UpdateArgs ua) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* red = reinterpret_cast<double*>(smem);        // [RED_NT]
+  int* flag = reinterpret_cast<int*>(red + RED_NT);      // [4]
+  double* upd = red + RED_NT + 2;                        // fused-update scratch
+
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int r = t >> 6;
+  const int o = blockIdx.x * 64 + l;
+  const int64_t lo = n_parts * blockIdx.y / NSLICE;
+  const int64_t hi = n_parts * (blockIdx.y + 1) / NSLICE;
+  double s = 0.0;
+  if (o < n_out)
+    for (int64_t b = lo + r; b < hi; b += 4) s += partials[b * n_out + o];
+  red[t] = s;
+  __syncthreads();
+  if (r == 0 && o < n_out)
+    stage[(size_t)blockIdx.y * n_out + o] = ((red[l] + red[64 + l]) + red[128 + l]) + red[192 + l];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t total = gridDim.x * gridDim.y;
+    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == total - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  if (!flag[0]) return;
+  double* ab = fuse ? upd : nullptr;
+  for (int oo = t; oo < n_out; oo += RED_NT) {
+    double v = 0.0;
+    for (int sl = 0; sl < NSLICE; ++sl) v += stage[(size_t)sl * n_out + oo];
+    out[oo] = v;
+    if (fuse) ab[oo] = v;
+  }
+  if (t == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!fuse) return;
+  __syncthreads();
+  double* scratch = upd + ((n_out + 1) & ~1);
+  if (ua.tc_double)
+    basis_update_block<double>(ab, ua.H64, (double*)ua.Ht, (double*)ua.HHt, ua.F, ua.k, ua.KP, ua.l1,
+                               ua.l2, 1, ua.stats, scratch);
+  else
+    basis_update_block<float>(ab, ua.H64, (float*)ua.Ht, (float*)ua.HHt, ua.F, ua.k, ua.KP, ua.l1,
+                              ua.l2, 1, ua.stats, scratch);
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side: kernel selection, occupancy-derived grid, launches
+// ------------------------------------------------------------------------------------------------
+using PassFn = const void*;
+
+struct PassKernel {
+  PassFn fn;
+  int KP, NPW;
+  bool split;
+  size_t sx, sc;
+};
+
+template <typename TX, int KP, int NPW, bool SPLIT>
+static PassKernel make_pk() {
+  return PassKernel{reinterpret_cast<PassFn>(&mu_pass_kernel<TX, KP, NPW, SPLIT>), KP, NPW, SPLIT,
+                    sizeof(TX), sizeof(typename Compute<TX>::T)};
+}
+
+template <typename TX, int KP>
+static bool pick_kp(int np, PassKernel* out) {
+  if (np <= 1) { *out = make_pk<TX, KP, 1, true>(); return true; }
+  if (np == 2) { *out = make_pk<TX, KP, 2, true>(); return true; }
+  const int npw = (np + NWAVE - 1) / NWAVE;
+  if (npw <= 1) { *out = make_pk<TX, KP, 1, false>(); return true; }
+  if (npw <= 2) { *out = make_pk<TX, KP, 2, false>(); return true; }
+  if (npw <= 4) { *out = make_pk<TX, KP, 4, false>(); return true; }
+  return false;
+}
+
+template <typename TX>
+static bool pick_tx(int KP, int np, PassKernel* out) {
+  switch (KP) {
+    case 4: return pick_kp<TX, 4>(np, out);
+    case 8: return pick_kp<TX, 8>(np, out);
+    case 16: return pick_kp<TX, 16>(np, out);
+  }
+  return false;
+}
+
+static int padded_k(int k) { return k <= 4 ? 4 : (k <= 8 ? 8 : 16); }
+
+static constexpr size_t kMaxLds = 160 * 1024;
+
+static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds) {
+  if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
+  if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
+  const int KP = padded_k(k);
+  const int np = (F + k + 63) / 64;
+  bool ok = false;
+  switch (x_dtype) {
+    case CNMF_F32: ok = pick_tx<float>(KP, np, pk); break;
+    case CNMF_F64: ok = pick_tx<double>(KP, np, pk); break;
+    case CNMF_BF16: ok = pick_tx<bf16_t>(KP, np, pk); break;
+    default: return set_err(CNMF_ERR_ARG, "unknown x_dtype %d", x_dtype);
+  }
+  if (!ok) return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d too wide for the pass kernel", F);
+  *lds = pass_lds(F, KP, pk->sx, pk->sc).total;
+  if (*lds > kMaxLds)
+    return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d needs %zu B of LDS per tile (> %zu)", F, *lds,
+                   kMaxLds);
+  return CNMF_OK;
+}
+
+struct OccKey {
+  int dev;
+  PassFn fn;
+  size_t lds;
+  bool operator==(const OccKey& o) const { return dev == o.dev && fn == o.fn && lds == o.lds; }
+};
+struct OccHash {
+  size_t operator()(const OccKey& k) const {
+    return std::hash<const void*>()(k.fn) ^ (k.lds * 1315423911u) ^ (size_t)k.dev;
+  }
+};
+static std::mutex g_occ_mu;
+static std::unordered_map<OccKey, int64_t, OccHash> g_occ;
+
+// max co-resident workgroups of this kernel on the current device (occupancy × CUs), cached
+static int64_t max_resident(PassFn fn, size_t lds) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  OccKey key{dev, fn, lds};
+  {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    auto it = g_occ.find(key);
+    if (it != g_occ.end()) return it->second;
+  }
+  if (lds > 64 * 1024)
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+      return -1;
+  int per_cu = 0, ncu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+  per_cu = std::max(1, std::min(per_cu, 8));
+  int64_t v = (int64_t)per_cu * ncu;
+  std::lock_guard<std::mutex> lk(g_occ_mu);
+  g_occ[key] = v;
+  return v;
+}
+
+static int64_t pass_grid(int64_t n_rows, PassFn fn, size_t lds) {
+  const int64_t n_tiles = (n_rows + TS - 1) / TS;
+  if (n_tiles == 0) return 0;
+  const int64_t maxb = max_resident(fn, lds);
+  if (maxb <= 0) return -1;
+  const int64_t rounds = (n_tiles + maxb - 1) / maxb;
+  return (n_tiles + rounds - 1) / rounds;
+}
+
+static size_t reduce_lds(int n_out, int fuse, int F, int k) {
+  size_t d = RED_NT + 2;
+  if (fuse) d += ((size_t)(n_out + 1) & ~size_t(1)) + update_lds_doubles(F, k, padded_k(k));
+  return d * sizeof(double);
+}
+
+}  // namespace cnmf
+
+using namespace cnmf;
+
+extern "C" {
+
+int cnmf_abi_version(void) { return 100; }
+
+const char* cnmf_last_error(void) { return g_err; }
+
+int cnmf_padded_k(int k) { return (k < 1 || k > 16) ? -1 : padded_k(k); }
+
+int64_t cnmf_stage_doubles(int n_out) { return (int64_t)NSLICE * (n_out > 0 ? n_out : 1); }
+
+int64_t cnmf_pass_blocks(int64_t n_rows, int n_features, int k, int x_dtype) {
+  if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
+  PassKernel pk;
+  size_t lds = 0;
+  int st = select_pass(x_dtype, n_features, k, &pk, &lds);
+  if (st) return st;
+  int64_t nb = pass_grid(n_rows, pk.fn, lds);
+  if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed (no HIP device?)");
+  return nb;
+}
+
+int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, const void* HHt,
+                        double* partials, int64_t n_rows, int n_features, int k, double l1_W,
+                        double l2_W, int flags, void* stream) {
+  if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
+  if (!X || !W || !Ht || !HHt) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  const int valid = CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE | CNMF_PASS_LOSS;
+  if ((flags & ~valid) || flags == 0 || ((flags & CNMF_PASS_LOSS) && flags != CNMF_PASS_LOSS) ||
+      ((flags & CNMF_PASS_ACCUMULATE) && !(flags & CNMF_PASS_UPDATE_W)))
+    return set_err(CNMF_ERR_ARG, "invalid flags %d", flags);
+  if ((flags & (CNMF_PASS_ACCUMULATE | CNMF_PASS_LOSS)) && !partials)
+    return set_err(CNMF_ERR_ARG, "partials required");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+  PassKernel pk;
+  size_t lds = 0;
+  int st = select_pass(x_dtype, n_features, k, &pk, &lds);
+  if (st) return st;
+  const int64_t nb = pass_grid(n_rows, pk.fn, lds);
+  if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (nb == 0) return CNMF_OK;
+  const int64_t n_tiles = (n_rows + TS - 1) / TS;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int F = n_features;
+  if (pk.sc == sizeof(double)) {
+    double l1 = l1_W, l2 = l2_W;
+    void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1, &l2, &flags, (void*)&n_tiles};
+    HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
+  } else {
+    float l1 = (float)l1_W, l2 = (float)l2_W;
+    void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1, &l2, &flags, (void*)&n_tiles};
+    HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
+  }
+  return CNMF_OK;
+}
+
+static int launch_reduce(const double* partials, int64_t n_parts, int n_out, double* stage,
+                         uint32_t* counter, double* out, int fuse, UpdateArgs ua, hipStream_t s) {
+  if (!stage || !counter || !out || (n_parts > 0 && !partials))
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_out < 1 || n_parts < 0) return set_err(CNMF_ERR_SHAPE, "invalid reduce shape");
+  const size_t lds = reduce_lds(n_out, fuse, ua.F, ua.k);
+  if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the fused update");
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&reduce_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  dim3 grid((unsigned)((n_out + 63) / 64), NSLICE);
+  hipLaunchKernelGGL(reduce_kernel, grid, dim3(RED_NT), lds, s, partials, n_parts, n_out, stage,
+                     counter, out, fuse, ua);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_reduce_partials(const double* partials, int64_t n_parts, int n_out, double* stage,
+                         uint32_t* counter, double* out, void* stream) {
+  UpdateArgs ua{};
+  ua.F = 1;
+  ua.k = 1;
+  return launch_reduce(partials, n_parts, n_out, stage, counter, out, 0, ua,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+static int check_update_args(const double* H64, const void* Ht, const void* HHt, int w_dtype, int F,
+                             int k) {
+  if (!H64 || !Ht || !HHt) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
+  if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
+  if (w_dtype != CNMF_F32 && w_dtype != CNMF_F64) return set_err(CNMF_ERR_ARG, "w_dtype must be F32/F64");
+  return CNMF_OK;
+}
+
+int cnmf_basis_update(const double* AB, double* H64, void* Ht, void* HHt, int w_dtype,
+                      int n_features, int k, double l1_H, double l2_H, int do_update,
+                      double* stats, void* stream) {
+  int st = check_update_args(H64, Ht, HHt, w_dtype, n_features, k);
+  if (st) return st;
+  if (do_update && !AB) return set_err(CNMF_ERR_ARG, "AB required for do_update");
+  const int KP = padded_k(k);
+  const size_t lds = update_lds_doubles(n_features, k, KP) * sizeof(double);
+  if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the update kernel");
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (w_dtype == CNMF_F64) {
+    if (lds > 64 * 1024)
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&basis_update_kernel<double>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(basis_update_kernel<double>, dim3(1), dim3(RED_NT), lds, s, AB, H64,
+                       (double*)Ht, (double*)HHt, n_features, k, KP, l1_H, l2_H, do_update, stats);
+  } else {
+    if (lds > 64 * 1024)
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&basis_update_kernel<float>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(basis_update_kernel<float>, dim3(1), dim3(RED_NT), lds, s, AB, H64,
+                       (float*)Ht, (float*)HHt, n_features, k, KP, l1_H, l2_H, do_update, stats);
+  }
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                       double* AB, double* H64, void* Ht, void* HHt, int w_dtype, int n_features,
+                       int k, double l1_H, double l2_H, double* stats, void* stream) {
+  int st = check_update_args(H64, Ht, HHt, w_dtype, n_features, k);
+  if (st) return st;
+  UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats, w_dtype == CNMF_F64};
+  return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, void* Ht,
+                       void* HHt, double* partials, int64_t n_parts, double* stage,
+                       uint32_t* counter, double* AB, double* stats, int64_t n_rows,
+                       int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
+                       void* const* pass_events, void* stream) {
+  const int w_dtype = x_dtype == CNMF_F64 ? CNMF_F64 : CNMF_F32;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  for (int it = 0; it < n_iter; ++it) {
+    if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it]), hs));
+    int st = cnmf_mu_sample_pass(X, x_dtype, W, Ht, HHt, partials, n_rows, n_features, k, l1_W,
+                                 l2_W, CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE, stream);
+    if (st) return st;
+    if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it + 1]), hs));
+    st = cnmf_reduce_update(partials, n_parts, stage, counter, AB, H64, Ht, HHt, w_dtype,
+                            n_features, k, l1_H, l2_H, stats, stream);
+    if (st) return st;
+  }
+  return CNMF_OK;
+}
+
+}  // extern "C"

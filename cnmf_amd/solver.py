@@ -1,0 +1,193 @@
+"""Host orchestration of the MU hot path on PyTorch-ROCm device memory.
+
+`MUPlan` owns the device buffers of one (shard of a) factorisation and issues the C-ABI launches;
+`run_mu` is the driver loop of sklearn's `_fit_multiplicative_update` (SK:731-893, loop SK:831-884):
+W then H every iteration, the Frobenius error every 10 iterations when tol > 0, and the relative
+decrease test (SK:872-884).  Iterations between two error checks go to the library in one call
+(`cnmf_mu_iterations`) — no host synchronisation inside a stretch.
+
+Multi-GPU: the rows of X/W are sharded over the ranks of a torch.distributed
+group; after each rank's pass, the per-rank fp64 accumulators [WᵀX | WᵀW] (k·(F+k) doubles) are
+summed with ONE all_reduce (RCCL over xGMI for backend "nccl"), and every rank applies the identical
+basis update.  The error check all-reduces one double.
+
+SK:<line> = sklearn/decomposition/_nmf.py (1.7.2).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check
+
+_XDT = {torch.float32: _lib.F32, torch.float64: _lib.F64, torch.bfloat16: _lib.BF16}
+
+
+def _ptr(t: torch.Tensor | None):
+    return None if t is None else t.data_ptr()
+
+
+def _event_array(events, n_iter):
+    if events is None:
+        return None
+    if len(events) != 2 * n_iter:
+        raise ValueError("pass_events must hold 2*n_iter events")
+    handles = [int(e.cuda_event) for e in events]
+    if not all(handles):
+        raise ValueError("record each event once before passing it (creates the HIP event)")
+    return (ctypes.c_void_p * len(handles))(*handles)
+
+
+class MUPlan:
+    """Device state for the MU iterations on X (n_rows × F, samples-major, already on the GPU)."""
+
+    def __init__(self, X: torch.Tensor, n_components: int, l1_W=0.0, l2_W=0.0, l1_H=0.0,
+                 l2_H=0.0, group=None):
+        if X.device.type != "cuda":
+            raise ValueError("MUPlan needs X on a HIP device")
+        if X.dtype not in _XDT:
+            raise TypeError(f"unsupported X dtype {X.dtype}")
+        if X.dim() != 2:
+            raise ValueError("X must be 2-D")
+        self.lib = _lib.load()
+        self.X = X.contiguous()
+        self.device = X.device
+        self.n_rows, self.F = (int(s) for s in self.X.shape)
+        self.k = int(n_components)
+        self.xdt = _XDT[X.dtype]
+        self.tc = torch.float64 if X.dtype == torch.float64 else torch.float32
+        self.wdt = _lib.F64 if self.tc == torch.float64 else _lib.F32
+        self.l1_W, self.l2_W, self.l1_H, self.l2_H = map(float, (l1_W, l2_W, l1_H, l2_H))
+        self.group = group
+        self.world = 1
+        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.world = torch.distributed.get_world_size(group)
+        KP = self.lib.cnmf_padded_k(self.k)
+        if KP < 0:
+            raise _lib.HipLibraryError(f"n_components={self.k} is not supported (1..16)")
+        self.KP = KP
+        self.V = self.F + self.k
+        self.n_out = self.k * self.V
+        with torch.cuda.device(self.device):
+            nb = self.lib.cnmf_pass_blocks(self.n_rows, self.F, self.k, self.xdt)
+        check(nb, "cnmf_pass_blocks")
+        self.n_parts = int(nb)
+        dev, f64 = self.device, torch.float64
+        self.W = torch.empty((self.n_rows, self.k), dtype=self.tc, device=dev)
+        self.H64 = torch.zeros((self.k, self.F), dtype=f64, device=dev)
+        self.Ht = torch.zeros((self.F, KP), dtype=self.tc, device=dev)
+        self.HHt = torch.zeros((KP, KP), dtype=self.tc, device=dev)
+        self.partials = torch.zeros((max(self.n_parts, 1), self.n_out), dtype=f64, device=dev)
+        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out)), dtype=f64, device=dev)
+        self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
+        self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
+        self.stats = torch.zeros(2, dtype=f64, device=dev)
+
+    # -- plumbing ------------------------------------------------------------------------------
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def set_W(self, W):
+        self.W.copy_(torch.as_tensor(W).to(device=self.device, dtype=self.tc))
+
+    def set_H(self, H):
+        """Load H (k × F) into the fp64 master copy and derive Ht/HHt (no update)."""
+        self.H64.copy_(torch.as_tensor(H).to(device=self.device, dtype=torch.float64))
+        self.refresh_basis()
+
+    def refresh_basis(self):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_basis_update(None, _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                                             self.wdt, self.F, self.k, 0.0, 0.0, 0, None,
+                                             self._stream()), "cnmf_basis_update")
+
+    # -- launches ------------------------------------------------------------------------------
+    def sample_pass(self, flags: int):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_mu_sample_pass(
+                _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self.partials), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, flags,
+                self._stream()), "cnmf_mu_sample_pass")
+
+    def reduce(self, n_out: int, out: torch.Tensor):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_reduce_partials(_ptr(self.partials), self.n_parts, n_out,
+                                                _ptr(self.stage), _ptr(self.counter), _ptr(out),
+                                                self._stream()), "cnmf_reduce_partials")
+
+    def basis_update(self):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_basis_update(_ptr(self.AB), _ptr(self.H64), _ptr(self.Ht),
+                                             _ptr(self.HHt), self.wdt, self.F, self.k, self.l1_H,
+                                             self.l2_H, 1, _ptr(self.stats), self._stream()),
+                  "cnmf_basis_update")
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+
+    def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
+        """n_iter MU iterations (SK:831-870) without host synchronisation.  pass_events: optional
+        list of 2*n_iter recorded-once torch.cuda.Event(enable_timing=True) bracketing each pass
+        (single GPU only)."""
+        if n_iter <= 0:
+            return
+        if not update_H:
+            for _ in range(n_iter):  # transform: W only, H (and Ht/HHt) fixed (SK:854 skipped)
+                self.sample_pass(_lib.PASS_UPDATE_W)
+            return
+        if self.world == 1:
+            with torch.cuda.device(self.device):
+                check(self.lib.cnmf_mu_iterations(
+                    n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
+                    _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
+                    _ptr(self.counter), _ptr(self.AB), _ptr(self.stats), self.n_rows, self.F, self.k,
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _event_array(pass_events, n_iter),
+                    self._stream()), "cnmf_mu_iterations")
+            return
+        for _ in range(n_iter):
+            self.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+            self.reduce(self.n_out, self.AB)
+            self._allreduce(self.AB)
+            self.basis_update()
+
+    def frobenius_error(self) -> float:
+        """sqrt(‖X − W·H‖²) over all ranks (SK:85-129 with square_root=True); synchronises."""
+        self.sample_pass(_lib.PASS_LOSS)
+        self.reduce(1, self.loss_buf)
+        self._allreduce(self.loss_buf)
+        return math.sqrt(max(float(self.loss_buf.item()), 0.0))
+
+    def H(self, dtype=None) -> torch.Tensor:
+        return self.H64.to(dtype or self.tc)
+
+
+def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool = True,
+           verbose: int = 0, return_errors: bool = False):
+    """The driver of `_fit_multiplicative_update` (SK:731-893).  Returns n_iter (and the error
+    trajectory [(n_iter, error)] when return_errors)."""
+    errors = []
+    if tol > 0:
+        error_at_init = plan.frobenius_error()  # SK:827
+        previous_error = error_at_init
+        errors.append((0, error_at_init))
+    it = 0
+    while it < max_iter:
+        stop = min(max_iter, (it // 10 + 1) * 10) if tol > 0 else max_iter
+        plan.iterate(stop - it, update_H)
+        it = stop
+        if tol > 0 and it % 10 == 0:  # SK:872-884
+            error = plan.frobenius_error()
+            errors.append((it, error))
+            if verbose:
+                print(f"Epoch {it:02d} reached, error: {error:f}")
+            if (previous_error - error) / error_at_init < tol:
+                break
+            previous_error = error
+    if return_errors:
+        return it, errors
+    return it

@@ -1,0 +1,110 @@
+/*
+ * cnmf_hip.h — C ABI of libcnmf_hip.so, the MI355X (gfx950) multiplicative-update hot path.
+ *
+ * The reference (AI-for-Ocean-Science/cnmf v1) has no solver and no FFI: its package
+ * `cnmf/__init__.py` is 0 bytes.  The arithmetic these entry points replace is the
+ * Frobenius multiplicative update of scikit-learn 1.7.2 (the reference's declared dependency,
+ * /root/reference/setup.py:26,30), cited below as SK:<line> = sklearn/decomposition/_nmf.py.
+ * Each entry point names the SK lines it takes over; INTEGRATION.md shows the ctypes binding.
+ *
+ * Layout (sklearn naming, samples-major): X[N][F] row-major, W[N][k], H[k][F].
+ * The pass computes in the "compute type" TC of its X dtype: fp32 for CNMF_F32 and CNMF_BF16,
+ * fp64 for CNMF_F64.  Basis-side state is fp64 (H64) with TC copies for the pass:
+ *   Ht [F][KP]  = H transposed, zero-padded to KP = cnmf_padded_k(k) columns
+ *   HHt[KP][KP] = H·Hᵀ (from fp64 H), zero-padded.
+ *   AB [k][F+k] = the reduced accumulators: AB[j][f] = (WᵀX)[j][f], AB[j][F+m] = (WᵀW)[j][m].
+ *
+ * Conventions.  All pointers are caller-owned device pointers (no allocation in any call except
+ * the one-off occupancy query); every launch is asynchronous on `stream` (a hipStream_t, NULL = the
+ * default stream); entry points return 0 or a negative cnmf_status and set a thread-local
+ * message readable with cnmf_last_error().  Re-entrant; no global mutable state except that
+ * message and a per-device occupancy cache.
+ */
+#ifndef CNMF_HIP_H
+#define CNMF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum cnmf_status {
+  CNMF_OK = 0,
+  CNMF_ERR_ARG = -1,         /* null pointer / bad flag / bad dtype                         */
+  CNMF_ERR_SHAPE = -2,       /* n_rows < 0, F < 1, k < 1                                    */
+  CNMF_ERR_UNSUPPORTED = -3, /* k > 16 or a row too wide for one LDS tile                   */
+  CNMF_ERR_ALIGN = -4,       /* X or W not 16-byte aligned                                  */
+  CNMF_ERR_HIP = -5          /* a HIP runtime call failed (message has hipGetErrorString)   */
+};
+
+enum cnmf_dtype { CNMF_F32 = 0, CNMF_F64 = 1, CNMF_BF16 = 2 };
+
+enum cnmf_pass_flags {
+  CNMF_PASS_UPDATE_W = 1,   /* update W in place (SK:526-631)                                */
+  CNMF_PASS_ACCUMULATE = 2, /* accumulate Wᵀ_newX and Wᵀ_newW_new partials (SK:639-640)      */
+  CNMF_PASS_LOSS = 4        /* only: partial sums of ‖X − W·H‖² (SK:85-129), one per block   */
+};
+
+/* ABI version (major*100 + minor) and last error message of the calling thread. */
+int cnmf_abi_version(void);
+const char* cnmf_last_error(void);
+
+/* KP = 4, 8 or 16: the padded component count the kernels use for k (1 <= k <= 16). */
+int cnmf_padded_k(int k);
+
+/* Number of partial rows (= workgroups) cnmf_mu_sample_pass writes for this shape on the
+ * current device; size `partials` as cnmf_pass_blocks(...) * max(1, k*(F+k)) doubles.
+ * Negative on error (e.g. unsupported shape or no device). */
+int64_t cnmf_pass_blocks(int64_t n_rows, int n_features, int k, int x_dtype);
+
+/* Doubles needed by the cross-block reduction stage buffer for n_out outputs. */
+int64_t cnmf_stage_doubles(int n_out);
+
+/* One fused HBM pass over the samples (replaces SK:534-629 and the N-reductions of SK:639-640):
+ *   num = X·Hᵀ, den = W·HHᵀ (+l1_W) (+l2_W·W), den==0 -> float32 eps, W <- W·(num/den)
+ *   and, with CNMF_PASS_ACCUMULATE, per-workgroup fp64 partials of [WᵀX | WᵀW] using the NEW W,
+ *   written to partials[block][k*(F+k)].  With CNMF_PASS_LOSS alone it writes per-workgroup
+ *   partials of ‖X − W·H‖² (partials[block][0]) and changes nothing.
+ *   X: [n_rows][F] of x_dtype; W: [n_rows][k] of TC; Ht, HHt: TC as above. */
+int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, const void* HHt,
+                        double* partials, int64_t n_rows, int n_features, int k, double l1_W,
+                        double l2_W, int flags, void* stream);
+
+/* Deterministic fp64 column sum of partials[n_parts][n_out] into out[n_out]
+ * (fixed slice order; stage: cnmf_stage_doubles(n_out) doubles; counter: one zeroed uint32 that
+ * the kernel leaves zeroed). */
+int cnmf_reduce_partials(const double* partials, int64_t n_parts, int n_out, double* stage,
+                         uint32_t* counter, double* out, void* stream);
+
+/* The basis update on the reduced AB (replaces SK:639-726 after the reductions):
+ *   den = (WᵀW)·H (+l1_H) (+l2_H·H), den==0 -> float32 eps, H <- H·(WᵀX/den)   (do_update=1)
+ * then refreshes Ht and HHt (TC = w_dtype: CNMF_F32 or CNMF_F64) from the fp64 H64.  With
+ * do_update=0 it only derives Ht/HHt from H64 (first iteration, transform).  stats (may be NULL)
+ * receives {<AB_A, H>, <AB_B, H·Hᵀ>} for the cheap loss ‖X‖² − 2<A,H> + <B,HHᵀ>. */
+int cnmf_basis_update(const double* AB, double* H64, void* Ht, void* HHt, int w_dtype,
+                      int n_features, int k, double l1_H, double l2_H, int do_update,
+                      double* stats, void* stream);
+
+/* cnmf_reduce_partials followed, in the same launch (last-arriving workgroup), by
+ * cnmf_basis_update(do_update=1): the single-GPU iteration tail. */
+int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                       double* AB, double* H64, void* Ht, void* HHt, int w_dtype, int n_features,
+                       int k, double l1_H, double l2_H, double* stats, void* stream);
+
+/* n_iter single-GPU MU iterations (pass + reduce_update each) launched back to back with no host
+ * synchronisation: the body of SK:831-870 for tol == 0 stretches.  pass_events (may be NULL):
+ * 2*n_iter caller-created hipEvent_t recorded on `stream` right before / after each sample pass
+ * (live per-launch timing of the dominant kernel for the roofline report). */
+int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, void* Ht,
+                       void* HHt, double* partials, int64_t n_parts, double* stage,
+                       uint32_t* counter, double* AB, double* stats, int64_t n_rows,
+                       int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
+                       void* const* pass_events, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CNMF_HIP_H */

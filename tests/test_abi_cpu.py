@@ -1,0 +1,32 @@
+"""CPU-side checks of the C ABI: the library loads and exports every declared symbol; host-only
+helpers answer without a GPU; the error path is a status code + message, never a crash."""
+import pytest
+
+from cnmf_amd import _lib
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    declared = _lib.declared_symbols()
+    assert len(declared) >= 10
+    missing = [s for s in declared if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_host_helpers():
+    lib = _lib.load()
+    assert lib.cnmf_abi_version() >= 100
+    assert [lib.cnmf_padded_k(k) for k in (1, 4, 5, 8, 9, 16)] == [4, 4, 8, 8, 16, 16]
+    assert lib.cnmf_padded_k(17) < 0 and lib.cnmf_padded_k(0) < 0
+    assert lib.cnmf_stage_doubles(340) == 16 * 340
+
+
+def test_error_paths_return_status():
+    lib = _lib.load()
+    st = lib.cnmf_mu_sample_pass(None, 0, None, None, None, None, 10, 81, 4, 0.0, 0.0, 3, None)
+    assert st == -1
+    assert b"null" in lib.cnmf_last_error()
+    assert lib.cnmf_pass_blocks(100, 81, 17, 0) == -3  # k > 16 unsupported
+    assert lib.cnmf_pass_blocks(100, 81, 4, 9) == -1   # unknown dtype
+    with pytest.raises(_lib.HipLibraryError):
+        _lib.check(-3, "probe")

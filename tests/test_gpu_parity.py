@@ -1,0 +1,174 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and sklearn's golden vectors.
+
+Bar (north_star): W and H within 1e-5 relative Frobenius of the fp64 oracle run on IDENTICAL inputs
+(the fp32 inputs promoted to fp64).  fp64 inputs: 1e-9.  bf16 X: the oracle runs on the
+bf16-rounded values, same 1e-5 bar.  Iteration counts (tol > 0) must match exactly.
+"""
+import numpy as np
+import pytest
+
+from golden_io import load, names, rel_fro
+from oracle import mu_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL32 = 1e-5
+TOL64 = 1e-9
+
+
+def _api():
+    import cnmf_amd
+    return cnmf_amd
+
+
+def _oracle_inputs(case):
+    X = case["X"]
+    kw = case["kwargs"]
+    k = kw["n_components"]
+    regs = mu_ref.compute_regularization(X.shape[0], X.shape[1], kw.get("alpha_W", 0.0),
+                                         kw.get("alpha_H", "same"), kw.get("l1_ratio", 0.0))
+    update_H = kw.get("update_H", True)
+    if not update_H:
+        W0, H0 = mu_ref.transform_init(X, k), case["H0"]
+    elif kw["init"] == "random":
+        from cnmf_amd.synthetic import random_init
+        W0, H0 = random_init(X, k, kw.get("random_state"))
+    else:
+        W0, H0 = case["W0"], case["H0"]
+    return X, W0, H0, regs, update_H
+
+
+@pytest.mark.parametrize("name", names())
+def test_golden_case_through_api(name):
+    cnmf_amd = _api()
+    case = load(name)
+    kw = dict(case["kwargs"])
+    X = case["X"]
+    W0 = case.get("W0")
+    H0 = case.get("H0")
+    W, H, n_iter = cnmf_amd.factorise(X, None if W0 is None else W0.copy(),
+                                      None if H0 is None else H0.copy(), **kw)
+    assert W.dtype == X.dtype and H.dtype == X.dtype
+    assert n_iter == case["n_iter"]
+    Xo, W0o, H0o, regs, update_H = _oracle_inputs(case)
+    Wr, Hr, nr = mu_ref.mu_fit(Xo.astype(np.float64), W0o.astype(np.float64), H0o.astype(np.float64),
+                               max_iter=kw["max_iter"], tol=kw["tol"], l1_reg_W=regs[0],
+                               l1_reg_H=regs[1], l2_reg_W=regs[2], l2_reg_H=regs[3],
+                               update_H=update_H)
+    tol = TOL64 if X.dtype == np.float64 else TOL32
+    ew, eh = rel_fro(W, Wr), rel_fro(H, Hr)
+    assert ew <= tol and eh <= tol, (name, ew, eh)
+    # and against sklearn's own outputs on the same inputs (fp32 sklearn drifts from fp64 itself)
+    ref_tol = TOL64 if X.dtype == np.float64 else 5e-5
+    assert rel_fro(W, case["W"]) <= ref_tol and rel_fro(H, case["H"]) <= ref_tol
+
+
+def test_single_pass_matches_numpy():
+    """One fused pass: W update and the [WᵀX | WᵀW] partial sums vs NumPy fp64 (ragged N, k=5)."""
+    import torch
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd import _lib
+    rng = np.random.default_rng(3)
+    N, F, k = 1000 + 37, 81, 5
+    X = rng.random((N, F)).astype(np.float32)
+    X[7] = 0.0
+    W0 = rng.random((N, k)).astype(np.float32)
+    H0 = rng.random((k, F)).astype(np.float32)
+    plan = MUPlan(torch.from_numpy(X).cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+    plan.reduce(plan.n_out, plan.AB)
+    torch.cuda.synchronize()
+    Xd, Wd, Hd = X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64)
+    Wref, _, _ = mu_ref.update_w(Xd, Wd.copy(), Hd)
+    Wg = plan.W.cpu().numpy()
+    assert rel_fro(Wg, Wref) < 1e-6
+    AB = plan.AB.cpu().numpy().reshape(k, F + k)
+    Wn = Wg.astype(np.float64)
+    np.testing.assert_allclose(AB[:, :F], Wn.T @ Xd, rtol=2e-6)
+    np.testing.assert_allclose(AB[:, F:], Wn.T @ Wn, rtol=2e-6)
+
+
+def test_loss_pass_matches_numpy():
+    import torch
+    from cnmf_amd.solver import MUPlan
+    rng = np.random.default_rng(4)
+    N, F, k = 777, 81, 4
+    X = rng.random((N, F)).astype(np.float32)
+    W0 = rng.random((N, k)).astype(np.float32)
+    H0 = rng.random((k, F)).astype(np.float32)
+    plan = MUPlan(torch.from_numpy(X).cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    err = plan.frobenius_error()
+    ref = mu_ref.frobenius_error(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64))
+    assert abs(err - ref) / ref < 1e-6
+
+
+@pytest.mark.parametrize("dt", ["float32", "float64"])
+def test_mid_size_500_iters(dt):
+    """1e5 x 81, k=4, 500 fixed iterations (cfg2's shape class at an oracle-friendly size)."""
+    cnmf_amd = _api()
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(100_000, 81, seed=0, dtype=np.dtype(dt))
+    W0, H0 = random_init(X, 4, 42)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom", tol=0.0,
+                                 max_iter=500)
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=500, tol=0.0)
+    tol = TOL32 if dt == "float32" else TOL64
+    assert rel_fro(W, Wr) <= tol and rel_fro(H, Hr) <= tol, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_k8_500_iters_fp32():
+    cnmf_amd = _api()
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(50_000, 81, seed=2, dtype=np.float32)
+    W0, H0 = random_init(X, 8, 42)
+    W, H, _ = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=8, init="custom", tol=0.0,
+                                 max_iter=500)
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=500, tol=0.0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_bf16_input_matches_oracle_on_rounded_values():
+    import torch
+    cnmf_amd = _api()
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X32 = iop_spectra(20_000, 300, seed=2, dtype=np.float32)
+    Xb = torch.from_numpy(X32).to(torch.bfloat16)
+    Xr = Xb.float().numpy()  # the values bf16 actually holds
+    W0, H0 = random_init(Xr, 16, 42)
+    W, H, _ = cnmf_amd.factorise(Xb.cuda(), torch.from_numpy(W0).cuda(), torch.from_numpy(H0).cuda(),
+                                 n_components=16, init="custom", tol=0.0, max_iter=50)
+    Wr, Hr, _ = mu_ref.mu_fit(Xr.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=50, tol=0.0)
+    assert rel_fro(W.cpu().numpy(), Wr) <= TOL32 and rel_fro(H.cpu().numpy(), Hr) <= TOL32
+
+
+def test_full_size_properties():
+    """cfg2 at full size (1e6 x 81, k=4): determinism, non-negativity, monotone objective."""
+    import torch
+    from cnmf_amd.solver import MUPlan, run_mu
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1_000_000, 81, seed=0, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    Xd = torch.from_numpy(X).cuda()
+    errs = []
+    outs = []
+    for rep in range(2):
+        plan = MUPlan(Xd, 4)
+        plan.set_W(torch.from_numpy(W0))
+        plan.set_H(torch.from_numpy(H0))
+        prev = plan.frobenius_error()
+        for _ in range(5):
+            run_mu(plan, max_iter=10, tol=0.0)
+            e = plan.frobenius_error()
+            assert e <= prev * (1 + 1e-7)
+            prev = e
+        errs.append(prev)
+        outs.append((plan.W.clone(), plan.H64.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert bool((outs[0][0] >= 0).all()) and bool((outs[0][1] >= 0).all())

@@ -452,13 +452,15 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
   double* sHH = sB + (size_t)k * k;  // [KP][KP]
   double* sR = sHH + (size_t)KP * KP;  // [2][RED_NT]
 
-  for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
+  const bool have_ab = AB != nullptr;  // NULL when only deriving Ht/HHt from H64 (do_update=0)
+  if (have_ab)
+    for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
   __syncthreads();
   for (int e = t; e < k * F; e += RED_NT) {
     const int j = e / F;
     const int f = e - j * F;
     double h = H64[e];
-    if (do_update) {
+    if (do_update && have_ab) {
       const double num = AB[j * V + f];                       // (WᵀX)[j][f], SK:639
       double den = 0.0;                                       // ((WᵀW)·H)[j][f], SK:640
       for (int m = 0; m < k; ++m) den = fma(sB[j * k + m], H64[m * F + f], den);
@@ -485,7 +487,7 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
     sHH[e] = v;
     HHt[e] = (TC)v;
   }
-  if (stats) {
+  if (stats && have_ab) {
     __syncthreads();
     double a = 0.0, b = 0.0;
     for (int e = t; e < k * F; e += RED_NT) a = fma(AB[(e / F) * V + (e % F)], sH[e], a);

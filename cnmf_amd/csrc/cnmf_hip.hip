@@ -47,7 +47,7 @@ constexpr int TS = 64;       // samples per tile
 constexpr int NT = 256;      // threads per workgroup
 constexpr int NWAVE = NT / 64;
 constexpr int PF = 8;        // 16-byte chunks per thread held in registers for the next tile
-constexpr int NSLICE = 16;   // slices of the deterministic cross-block reduction
+constexpr int NSLICE = 64;   // max slices of the deterministic cross-block reduction
 constexpr int RED_NT = 256;  // threads of the reduce / update workgroups
 constexpr double EPS32 = 1.1920928955078125e-07;  // np.finfo(np.float32).eps, SK:39
 
@@ -75,6 +75,9 @@ struct bf16_t {
   uint16_t bits;
 };
 
+// native 16-byte vector (HIP's uint4 class type defeats SROA: the prefetch array went to scratch)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float to_c(float v) { return v; }
 __device__ __forceinline__ double to_c(double v) { return v; }
 __device__ __forceinline__ float to_c(bf16_t v) { return __uint_as_float(((uint32_t)v.bits) << 16); }
@@ -96,26 +99,32 @@ struct Compute<bf16_t> {
 
 __host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
-// LDS carve of the pass kernel (bytes); identical on host and device.
+// LDS carve of the pass kernel (bytes); identical on host and device.  Every offset is 16-aligned.
 struct PassLds {
-  size_t region0;  // X tile, later reused for the cross-wave reduction
+  size_t region0;  // X tile [TS][F] (+4 zero elements), later the cross-wave reduction scratch
   size_t w;        // old-W tile, flat [ns][k]
-  size_t wn;       // new-W tile, [TS][KP]
+  size_t wn;       // new-W tile, [TS][KP] (zero for j >= k and for invalid samples)
   size_t p;        // partial num, [NWAVE][TS][KP]
+  size_t ht;       // Ht, [4*q][KP], rows >= F zero (q = ceil(F/4): each wave owns q features)
   size_t hht;      // HHt, [KP][KP]
+  size_t zero;     // 16 zero bytes (source of the idle lanes of the A phase)
   size_t total;
 };
 
+__host__ __device__ inline int feat_per_wave(int F) { return (F + NWAVE - 1) / NWAVE; }
+
 __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc) {
   PassLds L;
-  size_t xb = align16((size_t)TS * F * sx);
+  size_t xb = align16(((size_t)TS * F + 4) * sx);
   size_t rb = (size_t)NWAVE * 64 * KP * sizeof(double);
   L.region0 = xb > rb ? xb : rb;
   L.w = L.region0;
   L.wn = L.w + align16((size_t)TS * KP * sc);
   L.p = L.wn + align16((size_t)TS * KP * sc);
-  L.hht = L.p + align16((size_t)NWAVE * TS * KP * sc);
-  L.total = L.hht + align16((size_t)KP * KP * sc);
+  L.ht = L.p + align16((size_t)NWAVE * TS * KP * sc);
+  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sc);
+  L.zero = L.hht + align16((size_t)KP * KP * sc);
+  L.total = L.zero + 16;
   return L;
 }
 
@@ -123,11 +132,11 @@ __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc)
 struct TileGeom {
   const unsigned char* xsrc;
   const unsigned char* wsrc;
-  int ns;        // valid samples
-  int nxf;       // full 16-byte chunks of X
-  int nch;       // full chunks of X + W
-  int rx;        // trailing X elements (partial chunk)
-  int rw;        // trailing W elements
+  int ns;   // valid samples
+  int nxf;  // full 16-byte chunks of X
+  int nch;  // full chunks of X + W
+  int rx;   // trailing X elements (partial chunk)
+  int rw;   // trailing W elements
   int nwf;
 };
 
@@ -150,28 +159,57 @@ __device__ __forceinline__ TileGeom tile_geom(const TX* X, const TC* W, int64_t 
   return g;
 }
 
+template <typename T>
+__device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
+  return *reinterpret_cast<const T*>(smem + off);
+}
+
 // ------------------------------------------------------------------------------------------------
 // The fused sample pass.
 //   TX: X storage (float / double / bf16_t), TC: compute + W type, KP: padded k (4/8/16),
-//   NPW: 64-lane feature passes held in registers per wave, SPLIT: A phase splits the tile's
-//   samples over the 4 waves (few passes) or splits the passes over the waves (wide rows).
+//   FT: compile-time n_features (0 = runtime; the headline F=81 is specialised so every feature
+//   loop unrolls with immediate LDS offsets), NPW: 64-lane feature passes held in registers per
+//   wave, SPLIT: the A phase splits the tile's samples over the 4 waves (V <= 128) or splits the
+//   passes over the waves (wide rows).
+//
+// Per 64-sample tile (4 barriers):
+//   stage   prefetched registers -> LDS; issue the NEXT tile's 16-byte loads (in flight during the
+//           rest of this tile)
+//   phase 1 lane = sample, wave = quarter of the features: partial num[s][j] = Σ_f x[s][f]·Ht[f][j]
+//   phase 2 element (s, j): num = Σ_waves partial; den = Σ_m w[s][m]·HHt[m][j] (+l1)(+l2·w);
+//           den==0 -> eps32; w' = w·(num/den) -> HBM and LDS
+//   phase 3 lane = virtual feature v: acc[j][v] += w'[s][j]·[x | w'][s][v] (fp32 registers for
+//           the whole launch; combined across waves in fp64 at the end)
 // ------------------------------------------------------------------------------------------------
-template <typename TX, int KP, int NPW, bool SPLIT>
-__global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
+// minimum waves per SIMD the register allocator must leave room for (no spills; measured with
+// -Rpass-analysis=kernel-resource-usage): the F=81 fp32 k<=4 kernel fits 128 VGPRs (4 waves/SIMD)
+template <typename TX, int KP, int FT>
+constexpr int pass_min_waves() {
+  return FT == 0 ? ((KP == 16 || sizeof(TX) == 8) ? 1 : 2)
+                 : (KP == 4 ? (sizeof(TX) == 8 ? 3 : 4)
+                            : (KP == 8 ? (sizeof(TX) == 8 ? 2 : 3) : (sizeof(TX) == 8 ? 1 : 2)));
+}
+
+template <typename TX, int KP, int FT, int NPW, bool SPLIT>
+__global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_kernel(const TX* __restrict__ X,
                                                      typename Compute<TX>::T* __restrict__ W,
                                                      const typename Compute<TX>::T* __restrict__ Ht,
                                                      const typename Compute<TX>::T* __restrict__ HHt,
                                                      double* __restrict__ partials, int64_t n_rows,
-                                                     int F, int k, typename Compute<TX>::T l1,
+                                                     int F_rt, int k, typename Compute<TX>::T l1,
                                                      typename Compute<TX>::T l2, int flags,
                                                      int64_t n_tiles) {
   using TC = typename Compute<TX>::T;
+  constexpr bool SAME = sizeof(TX) == sizeof(TC);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int F = FT > 0 ? FT : F_rt;
+  const int q = feat_per_wave(F);
   const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC));
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
   TC* sP = reinterpret_cast<TC*>(smem + L.p);
+  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
   TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
@@ -184,25 +222,33 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
   const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
 
+  // basis-side constants into LDS once per launch (Ht zero-padded to 4q rows)
+  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : TC(0);
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
+  if (t < 4) {
+    sX[TS * F + t] = TX{};
+    reinterpret_cast<uint32_t*>(smem + L.zero)[t] = 0u;
+  }
 
-  double acc64[NPW][KP];
+  TC acc[NPW][KP];
 #pragma unroll
   for (int i = 0; i < NPW; ++i)
 #pragma unroll
-    for (int j = 0; j < KP; ++j) acc64[i][j] = 0.0;
+    for (int j = 0; j < KP; ++j) acc[i][j] = TC(0);
   double loss64 = 0.0;
 
-  uint4 pf[PF];
+  // 16-byte chunks per thread per tile: exact for a compile-time F, PF otherwise
+  constexpr int PFT = FT > 0 ? (int)((TS * FT * sizeof(TX) + TS * KP * sizeof(TC) + 16 * NT - 1) / (16 * NT)) : PF;
+  u32x4 pf[PFT];
   int64_t tile = blockIdx.x;
   if (tile < n_tiles) {
     TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
+    for (int i = 0; i < PFT; ++i) {
       int c = t + NT * i;
       if (c < g.nch) {
         const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
-        pf[i] = *reinterpret_cast<const uint4*>(src);
+        pf[i] = *reinterpret_cast<const u32x4*>(src);
       }
     }
   }
@@ -212,25 +258,29 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
     const int ns = g.ns;
     // ---- stage tile `tile` (prefetched registers + any overflow chunks + ragged tail) into LDS
 #pragma unroll
-    for (int i = 0; i < PF; ++i) {
+    for (int i = 0; i < PFT; ++i) {
       int c = t + NT * i;
       if (c < g.nch) {
         unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
-        *reinterpret_cast<uint4*>(dst) = pf[i];
+        *reinterpret_cast<u32x4*>(dst) = pf[i];
       }
     }
-    for (int c = t + NT * PF; c < g.nch; c += NT) {
+    for (int c = t + NT * PFT; c < g.nch; c += NT) {
       const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
       unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
-      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
     }
-    if (t < g.rx) {
-      int e = g.nxf * (16 / (int)sizeof(TX)) + t;
-      sX[e] = reinterpret_cast<const TX*>(g.xsrc)[e];
-    }
-    if (t >= 64 && t - 64 < g.rw) {
-      int e = g.nwf * (16 / (int)sizeof(TC)) + (t - 64);
-      sW[e] = reinterpret_cast<const TC*>(g.wsrc)[e];
+    if (ns < TS) {  // ragged last tile: element tails, and zeros after the last valid row so the
+                    // padded feature reads of phase 1 (Ht rows >= F are zero) never meet NaN bits
+      if (t < g.rx) {
+        int e = g.nxf * (16 / (int)sizeof(TX)) + t;
+        sX[e] = reinterpret_cast<const TX*>(g.xsrc)[e];
+      }
+      if (t >= 64 && t - 64 < g.rw) {
+        int e = g.nwf * (16 / (int)sizeof(TC)) + (t - 64);
+        sW[e] = reinterpret_cast<const TC*>(g.wsrc)[e];
+      }
+      if (t >= 128 && t - 128 < 4) sX[ns * F + (t - 128)] = TX{};
     }
     __syncthreads();
 
@@ -240,34 +290,33 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
       if (nt < n_tiles) {
         TileGeom gn = tile_geom(X, W, nt, n_rows, F, k);
 #pragma unroll
-        for (int i = 0; i < PF; ++i) {
+        for (int i = 0; i < PFT; ++i) {
           int c = t + NT * i;
           if (c < gn.nch) {
             const unsigned char* src =
                 c < gn.nxf ? gn.xsrc + 16 * (size_t)c : gn.wsrc + 16 * (size_t)(c - gn.nxf);
-            pf[i] = *reinterpret_cast<const uint4*>(src);
+            pf[i] = *reinterpret_cast<const u32x4*>(src);
           }
         }
       }
     }
 
-    // ---- phase 1: lane = sample, wave = quarter of the features
+    // ---- phase 1: lane = sample, wave = quarter of the (zero-padded) features
     {
-      const int q = (F + NWAVE - 1) / NWAVE;
       const int fb = wave * q;
-      const int fe = min(F, fb + q);
-      const TX* xr = sX + (size_t)lane * F;
+      const TX* xr = sX + (size_t)lane * F + fb;
+      const TC* hb = sHt + (size_t)fb * KP;
       if (do_loss) {
         TC w[KP];
 #pragma unroll
         for (int j = 0; j < KP; ++j) w[j] = (j < k && lane < ns) ? sW[lane * k + j] : TC(0);
+        const int nf = min(q, F - fb);
         TC part = 0;
-        for (int f = fb; f < fe; ++f) {
+        for (int f = 0; f < nf; ++f) {
           const TC xv = to_c(xr[f]);
-          const TC* hr = Ht + (size_t)f * KP;
           TC wh = 0;
 #pragma unroll
-          for (int j = 0; j < KP; ++j) wh = fma(w[j], hr[j], wh);
+          for (int j = 0; j < KP; ++j) wh = fma(w[j], hb[f * KP + j], wh);
           const TC r = xv - wh;
           part = fma(r, r, part);
         }
@@ -276,12 +325,21 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
         TC p[KP];
 #pragma unroll
         for (int j = 0; j < KP; ++j) p[j] = 0;
-#pragma unroll 4
-        for (int f = fb; f < fe; ++f) {
-          const TC xv = to_c(xr[f]);
-          const TC* hr = Ht + (size_t)f * KP;
+        if constexpr (FT > 0) {
+          constexpr int QF = (FT + NWAVE - 1) / NWAVE;
+#pragma unroll 7
+          for (int f = 0; f < QF; ++f) {
+            const TC xv = to_c(xr[f]);
 #pragma unroll
-          for (int j = 0; j < KP; ++j) p[j] = fma(xv, hr[j], p[j]);
+            for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+          }
+        } else {
+#pragma unroll 4
+          for (int f = 0; f < q; ++f) {
+            const TC xv = to_c(xr[f]);
+#pragma unroll
+            for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+          }
         }
 #pragma unroll
         for (int j = 0; j < KP; ++j) sP[(wave * TS + lane) * KP + j] = p[j];
@@ -298,13 +356,23 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
         const int j = e % KP;
         TC wn = 0;
         if (s < ns && j < k) {
-          const TC num = sP[(0 * TS + s) * KP + j] + sP[(1 * TS + s) * KP + j] +
-                         sP[(2 * TS + s) * KP + j] + sP[(3 * TS + s) * KP + j];
+          const TC num = ((sP[(0 * TS + s) * KP + j] + sP[(1 * TS + s) * KP + j]) +
+                          sP[(2 * TS + s) * KP + j]) + sP[(3 * TS + s) * KP + j];
           TC den = 0;
+          TC wold;
+          if (k == KP) {
+            TC wr[KP];
 #pragma unroll
-          for (int m = 0; m < KP; ++m)
-            if (m < k) den = fma(sW[s * k + m], sHHt[m * KP + j], den);
-          const TC wold = sW[s * k + j];
+            for (int m = 0; m < KP; ++m) wr[m] = sW[s * KP + m];
+#pragma unroll
+            for (int m = 0; m < KP; ++m) den = fma(wr[m], sHHt[m * KP + j], den);
+            wold = sW[s * KP + j];
+          } else {
+#pragma unroll
+            for (int m = 0; m < KP; ++m)
+              if (m < k) den = fma(sW[s * k + m], sHHt[m * KP + j], den);
+            wold = sW[s * k + j];
+          }
           if (l1 > TC(0)) den += l1;                    // SK:616-617
           if (l2 > TC(0)) den = den + l2 * wold;        // SK:618-619
           if (den == TC(0)) den = TC(EPS32);            // SK:620
@@ -318,41 +386,53 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
     }
 
     if (do_acc) {
-      // ---- phase 3: lane = virtual feature v (v < F: X column, F <= v < F+k: W_new column);
-      //      acc[j][v] += w_new[s][j] · value[s][v]   (the rows of [WᵀX | WᵀW], SK:639-640)
+      // ---- phase 3: lane = virtual feature v (v < F: X column, F <= v < F+k: W_new column,
+      //      beyond: a zero word); acc[j][v] += w_new[s][j]·value[s][v]  (SK:639-640)
       if (SPLIT) {
         const int s_beg = wave * (TS / NWAVE);
-        const int s_end = min(ns, s_beg + TS / NWAVE);
-        TC a32[NPW][KP];
+        const int nsw = min(max(ns - s_beg, 0), TS / NWAVE);
+        // per-lane byte offset / stride of each pass's source column
+        uint32_t offx[NPW], stx[NPW], offw[NPW], stw[NPW];
+        bool isx[NPW];
 #pragma unroll
-        for (int i = 0; i < NPW; ++i)
-#pragma unroll
-          for (int j = 0; j < KP; ++j) a32[i][j] = 0;
-        for (int s = s_beg; s < s_end; ++s) {
+        for (int i = 0; i < NPW; ++i) {
+          const int v = 64 * i + lane;
+          isx[i] = v < F;
+          offx[i] = (uint32_t)((size_t)s_beg * F + min(v, F - 1)) * sizeof(TX);
+          stx[i] = (uint32_t)(F * sizeof(TX));
+          const bool isw = v >= F && v < V;
+          offw[i] = isw ? (uint32_t)(L.wn + ((size_t)s_beg * KP + (v - F)) * sizeof(TC)) : (uint32_t)L.zero;
+          stw[i] = isw ? (uint32_t)(KP * sizeof(TC)) : 0u;
+        }
+        auto body = [&](int s) {
           TC wv[KP];
 #pragma unroll
-          for (int j = 0; j < KP; ++j) wv[j] = sWn[s * KP + j];
+          for (int j = 0; j < KP; ++j) wv[j] = sWn[(s_beg + s) * KP + j];
 #pragma unroll
           for (int i = 0; i < NPW; ++i) {
             if (i < np) {
-              const int v = 64 * i + lane;
               TC val;
               if (64 * i + 64 <= F) {
-                val = to_c(sX[(size_t)s * F + v]);
+                val = to_c(sX[(size_t)(s_beg + s) * F + 64 * i + lane]);
+              } else if constexpr (SAME) {
+                const uint32_t o = isx[i] ? offx[i] + s * stx[i] : offw[i] + s * stw[i];
+                val = lds_at<TC>(smem, o);
               } else {
-                const TC vx = to_c(sX[(size_t)s * F + min(v, F - 1)]);
-                const TC vw = sWn[s * KP + min(max(v - F, 0), KP - 1)];
-                val = v < F ? vx : (v < V ? vw : TC(0));
+                const TC vx = to_c(lds_at<TX>(smem, offx[i] + s * stx[i]));
+                const TC vw = lds_at<TC>(smem, offw[i] + s * stw[i]);
+                val = isx[i] ? vx : vw;
               }
 #pragma unroll
-              for (int j = 0; j < KP; ++j) a32[i][j] = fma(wv[j], val, a32[i][j]);
+              for (int j = 0; j < KP; ++j) acc[i][j] = fma(wv[j], val, acc[i][j]);
             }
           }
+        };
+        if (nsw == TS / NWAVE) {
+#pragma unroll 4
+          for (int s = 0; s < TS / NWAVE; ++s) body(s);
+        } else {
+          for (int s = 0; s < nsw; ++s) body(s);
         }
-#pragma unroll
-        for (int i = 0; i < NPW; ++i)
-#pragma unroll
-          for (int j = 0; j < KP; ++j) acc64[i][j] += (double)a32[i][j];
       } else {
 #pragma unroll
         for (int i = 0; i < NPW; ++i) {
@@ -360,9 +440,12 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
           if (p < np) {
             const int v = 64 * p + lane;
             const bool full = 64 * p + 64 <= F;
-            TC a32[KP];
-#pragma unroll
-            for (int j = 0; j < KP; ++j) a32[j] = 0;
+            const bool isx = v < F;
+            const uint32_t offx = (uint32_t)min(v, F - 1) * sizeof(TX);
+            const bool isw = v >= F && v < V;
+            const uint32_t offw = isw ? (uint32_t)(L.wn + (v - F) * sizeof(TC)) : (uint32_t)L.zero;
+            const uint32_t stw = isw ? (uint32_t)(KP * sizeof(TC)) : 0u;
+#pragma unroll 4
             for (int s = 0; s < ns; ++s) {
               TC wv[KP];
 #pragma unroll
@@ -371,15 +454,13 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
               if (full) {
                 val = to_c(sX[(size_t)s * F + v]);
               } else {
-                const TC vx = to_c(sX[(size_t)s * F + min(v, F - 1)]);
-                const TC vw = sWn[s * KP + min(max(v - F, 0), KP - 1)];
-                val = v < F ? vx : (v < V ? vw : TC(0));
+                const TC vx = to_c(lds_at<TX>(smem, offx + (uint32_t)(s * F * sizeof(TX))));
+                const TC vw = lds_at<TC>(smem, offw + s * stw);
+                val = isx ? vx : vw;
               }
 #pragma unroll
-              for (int j = 0; j < KP; ++j) a32[j] = fma(wv[j], val, a32[j]);
+              for (int j = 0; j < KP; ++j) acc[i][j] = fma(wv[j], val, acc[i][j]);
             }
-#pragma unroll
-            for (int j = 0; j < KP; ++j) acc64[i][j] += (double)a32[j];
           }
         }
       }
@@ -387,7 +468,7 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
     __syncthreads();  // LDS tiles are rewritten by the next iteration
   }
 
-  // ---- per-workgroup partial rows
+  // ---- per-workgroup partial rows (fp64 combine of the 4 waves' fp32 accumulators)
   if (do_acc) {
     const int n_out = k * V;
     double* prow = partials + (size_t)blockIdx.x * n_out;
@@ -397,15 +478,15 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
         if (i < np) {
           __syncthreads();
 #pragma unroll
-          for (int j = 0; j < KP; ++j) sRed[(wave * 64 + lane) * KP + j] = acc64[i][j];
+          for (int j = 0; j < KP; ++j) sRed[(wave * 64 + lane) * KP + j] = (double)acc[i][j];
           __syncthreads();
           for (int e = t; e < 64 * KP; e += NT) {
             const int l = e & 63;
             const int j = e >> 6;
             const int v = 64 * i + l;
             if (v < V && j < k) {
-              const double sum = sRed[(0 * 64 + l) * KP + j] + sRed[(1 * 64 + l) * KP + j] +
-                                 sRed[(2 * 64 + l) * KP + j] + sRed[(3 * 64 + l) * KP + j];
+              const double sum = ((sRed[(0 * 64 + l) * KP + j] + sRed[(1 * 64 + l) * KP + j]) +
+                                  sRed[(2 * 64 + l) * KP + j]) + sRed[(3 * 64 + l) * KP + j];
               prow[j * V + v] = sum;
             }
           }
@@ -419,7 +500,7 @@ __global__ __launch_bounds__(NT) void mu_pass_kernel(const TX* __restrict__ X,
         if (p < np && v < V) {
 #pragma unroll
           for (int j = 0; j < KP; ++j)
-            if (j < k) prow[j * V + v] = acc64[i][j];
+            if (j < k) prow[j * V + v] = (double)acc[i][j];
         }
       }
     }
@@ -523,7 +604,7 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
 
 // ------------------------------------------------------------------------------------------------
 // Deterministic fp64 reduction of partials[n_parts][n_out]; optional fused basis update.
-// grid = (ceil(n_out/64), NSLICE); the ticket-elected last workgroup sums the NSLICE stage rows.
+// grid = (ceil(n_out/64), nslice <= NSLICE); the ticket-elected last workgroup sums the stage rows.
 // ------------------------------------------------------------------------------------------------
 struct UpdateArgs {
   double* H64;
@@ -536,7 +617,7 @@ struct UpdateArgs {
 };
 
 __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict__ partials,
-                                                        int64_t n_parts, int n_out,
+                                                        int64_t n_parts, int n_out, int nslice,
                                                         double* __restrict__ stage,
                                                         uint32_t* __restrict__ counter,
                                                         double* __restrict__ out, int fuse,
@@ -550,11 +631,22 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
   const int l = t & 63;
   const int r = t >> 6;
   const int o = blockIdx.x * 64 + l;
-  const int64_t lo = n_parts * blockIdx.y / NSLICE;
-  const int64_t hi = n_parts * (blockIdx.y + 1) / NSLICE;
+  const int64_t lo = n_parts * blockIdx.y / nslice;
+  const int64_t hi = n_parts * (blockIdx.y + 1) / nslice;
+  // rows lo+r, lo+r+4, ... : up to 8 independent loads in flight per thread, fixed summation order
   double s = 0.0;
-  if (o < n_out)
-    for (int64_t b = lo + r; b < hi; b += 4) s += partials[b * n_out + o];
+  if (o < n_out) {
+    for (int64_t b0 = lo + r; b0 < hi; b0 += 32) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t b = b0 + 4 * u;
+        v[u] = b < hi ? partials[b * n_out + o] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+  }
   red[t] = s;
   __syncthreads();
   if (r == 0 && o < n_out)
@@ -578,7 +670,13 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
   double* ab = fuse ? upd : nullptr;
   for (int oo = t; oo < n_out; oo += RED_NT) {
     double v = 0.0;
-    for (int sl = 0; sl < NSLICE; ++sl) v += stage[(size_t)sl * n_out + oo];
+    for (int s0 = 0; s0 < nslice; s0 += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = s0 + u < nslice ? stage[(size_t)(s0 + u) * n_out + oo] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
     out[oo] = v;
     if (fuse) ab[oo] = v;
   }
@@ -595,6 +693,36 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
+// HBM read probe: the achievable streaming-read ceiling on this device (16-byte loads, 8 in flight
+// per lane, grid-stride; one fp64 checksum per workgroup so nothing is dead code).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void hbm_probe_kernel(const u32x4* __restrict__ buf, int64_t n16,
+                                                        double* __restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  uint32_t acc = 0;
+  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + 7 * stride < n16; i += 8 * stride) {
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(buf + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+  }
+  for (; i < n16; i += stride) {
+    u32x4 v = buf[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  __shared__ uint32_t red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t a = 0;
+    for (int j = 0; j < 256; ++j) a ^= red[j];
+    out[blockIdx.x] = (double)a;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // host side: kernel selection, occupancy-derived grid, launches
 // ------------------------------------------------------------------------------------------------
 using PassFn = const void*;
@@ -606,29 +734,30 @@ struct PassKernel {
   size_t sx, sc;
 };
 
-template <typename TX, int KP, int NPW, bool SPLIT>
+template <typename TX, int KP, int FT, int NPW, bool SPLIT>
 static PassKernel make_pk() {
-  return PassKernel{reinterpret_cast<PassFn>(&mu_pass_kernel<TX, KP, NPW, SPLIT>), KP, NPW, SPLIT,
+  return PassKernel{reinterpret_cast<PassFn>(&mu_pass_kernel<TX, KP, FT, NPW, SPLIT>), KP, NPW, SPLIT,
                     sizeof(TX), sizeof(typename Compute<TX>::T)};
 }
 
 template <typename TX, int KP>
-static bool pick_kp(int np, PassKernel* out) {
-  if (np <= 1) { *out = make_pk<TX, KP, 1, true>(); return true; }
-  if (np == 2) { *out = make_pk<TX, KP, 2, true>(); return true; }
+static bool pick_kp(int F, int np, PassKernel* out) {
+  if (F == 81 && np == 2) { *out = make_pk<TX, KP, 81, 2, true>(); return true; }  // IOP grid
+  if (np <= 1) { *out = make_pk<TX, KP, 0, 1, true>(); return true; }
+  if (np == 2) { *out = make_pk<TX, KP, 0, 2, true>(); return true; }
   const int npw = (np + NWAVE - 1) / NWAVE;
-  if (npw <= 1) { *out = make_pk<TX, KP, 1, false>(); return true; }
-  if (npw <= 2) { *out = make_pk<TX, KP, 2, false>(); return true; }
-  if (npw <= 4) { *out = make_pk<TX, KP, 4, false>(); return true; }
+  if (npw <= 1) { *out = make_pk<TX, KP, 0, 1, false>(); return true; }
+  if (npw <= 2) { *out = make_pk<TX, KP, 0, 2, false>(); return true; }
+  if (npw <= 4) { *out = make_pk<TX, KP, 0, 4, false>(); return true; }
   return false;
 }
 
 template <typename TX>
-static bool pick_tx(int KP, int np, PassKernel* out) {
+static bool pick_tx(int KP, int F, int np, PassKernel* out) {
   switch (KP) {
-    case 4: return pick_kp<TX, 4>(np, out);
-    case 8: return pick_kp<TX, 8>(np, out);
-    case 16: return pick_kp<TX, 16>(np, out);
+    case 4: return pick_kp<TX, 4>(F, np, out);
+    case 8: return pick_kp<TX, 8>(F, np, out);
+    case 16: return pick_kp<TX, 16>(F, np, out);
   }
   return false;
 }
@@ -644,9 +773,9 @@ static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds) {
   const int np = (F + k + 63) / 64;
   bool ok = false;
   switch (x_dtype) {
-    case CNMF_F32: ok = pick_tx<float>(KP, np, pk); break;
-    case CNMF_F64: ok = pick_tx<double>(KP, np, pk); break;
-    case CNMF_BF16: ok = pick_tx<bf16_t>(KP, np, pk); break;
+    case CNMF_F32: ok = pick_tx<float>(KP, F, np, pk); break;
+    case CNMF_F64: ok = pick_tx<double>(KP, F, np, pk); break;
+    case CNMF_BF16: ok = pick_tx<bf16_t>(KP, F, np, pk); break;
     default: return set_err(CNMF_ERR_ARG, "unknown x_dtype %d", x_dtype);
   }
   if (!ok) return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d too wide for the pass kernel", F);
@@ -779,9 +908,10 @@ static int launch_reduce(const double* partials, int64_t n_parts, int n_out, dou
   if (lds > 64 * 1024)
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&reduce_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  dim3 grid((unsigned)((n_out + 63) / 64), NSLICE);
-  hipLaunchKernelGGL(reduce_kernel, grid, dim3(RED_NT), lds, s, partials, n_parts, n_out, stage,
-                     counter, out, fuse, ua);
+  const int nslice = (int)std::max<int64_t>(1, std::min<int64_t>(NSLICE, (n_parts + 15) / 16));
+  dim3 grid((unsigned)((n_out + 63) / 64), (unsigned)nslice);
+  hipLaunchKernelGGL(reduce_kernel, grid, dim3(RED_NT), lds, s, partials, n_parts, n_out, nslice,
+                     stage, counter, out, fuse, ua);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }
@@ -839,6 +969,17 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
   UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats, w_dtype == CNMF_F64};
   return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,
                        reinterpret_cast<hipStream_t>(stream));
+}
+
+int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream) {
+  if (!buf || !out || bytes < 16 || n_blocks < 1)
+    return set_err(CNMF_ERR_ARG, "invalid hbm probe arguments");
+  if (reinterpret_cast<uintptr_t>(buf) & 15) return set_err(CNMF_ERR_ALIGN, "buf must be 16-byte aligned");
+  hipLaunchKernelGGL(hbm_probe_kernel, dim3(n_blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const u32x4*>(buf),
+                     bytes / 16, out);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
 }
 
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, void* Ht,

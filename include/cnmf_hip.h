@@ -103,6 +103,10 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
                        void* const* pass_events, void* stream);
 
+/* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
+ * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
+int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

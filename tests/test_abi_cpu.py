@@ -18,7 +18,7 @@ def test_host_helpers():
     assert lib.cnmf_abi_version() >= 100
     assert [lib.cnmf_padded_k(k) for k in (1, 4, 5, 8, 9, 16)] == [4, 4, 8, 8, 16, 16]
     assert lib.cnmf_padded_k(17) < 0 and lib.cnmf_padded_k(0) < 0
-    assert lib.cnmf_stage_doubles(340) == 16 * 340
+    assert lib.cnmf_stage_doubles(340) == 64 * 340
 
 
 def test_error_paths_return_status():

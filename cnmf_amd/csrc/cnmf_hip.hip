@@ -159,6 +159,21 @@ __device__ __forceinline__ TileGeom tile_geom(const TX* X, const TC* W, int64_t 
   return g;
 }
 
+// Issue this thread's 16-byte chunk loads of a tile.  Branch-free on purpose: chunks past the tile
+// re-read chunk 0 (an L1/L2 hit) instead of sitting in a divergent `if` — guarded loads made hipcc
+// put an `s_waitcnt vmcnt(0)` in front of every load, serialising the prefetch (and waiting on the
+// previous tile's W stores).
+template <int N>
+__device__ __forceinline__ void prefetch_tile(u32x4 (&pf)[N], const TileGeom& g, int t) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int c = t + NT * i;
+    const size_t off = c < g.nxf ? 16 * (size_t)c : (c < g.nch ? 16 * (size_t)(c - g.nxf) : 0);
+    const unsigned char* base = (c < g.nxf || c >= g.nch) ? g.xsrc : g.wsrc;
+    pf[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(base + off));
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
   return *reinterpret_cast<const T*>(smem + off);
@@ -243,14 +258,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   int64_t tile = blockIdx.x;
   if (tile < n_tiles) {
     TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
-#pragma unroll
-    for (int i = 0; i < PFT; ++i) {
-      int c = t + NT * i;
-      if (c < g.nch) {
-        const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
-        pf[i] = *reinterpret_cast<const u32x4*>(src);
-      }
-    }
+    prefetch_tile<PFT>(pf, g, t);
   }
 
   for (; tile < n_tiles; tile += gridDim.x) {
@@ -288,16 +296,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
     {
       const int64_t nt = tile + gridDim.x;
       if (nt < n_tiles) {
-        TileGeom gn = tile_geom(X, W, nt, n_rows, F, k);
-#pragma unroll
-        for (int i = 0; i < PFT; ++i) {
-          int c = t + NT * i;
-          if (c < gn.nch) {
-            const unsigned char* src =
-                c < gn.nxf ? gn.xsrc + 16 * (size_t)c : gn.wsrc + 16 * (size_t)(c - gn.nxf);
-            pf[i] = *reinterpret_cast<const u32x4*>(src);
-          }
-        }
+        prefetch_tile<PFT>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
       }
     }
 
@@ -519,7 +518,13 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
 // Basis update (one workgroup): the k×F epilogue, all in fp64.
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ inline size_t update_lds_doubles(int F, int k, int KP) {
-  return (size_t)k * F + (size_t)k * k + (size_t)KP * KP + RED_NT * 2;
+  return 2 * (size_t)k * F + (size_t)k * k + (size_t)KP * KP + 2 * (RED_NT / 64);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
 }
 
 template <typename TC>
@@ -527,24 +532,29 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
                                    int KP, double l1, double l2, int do_update, double* stats,
                                    double* lds) {
   const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  constexpr int NWV = RED_NT / 64;
   const int V = F + k;
-  double* sH = lds;               // [k][F] new H
-  double* sB = sH + (size_t)k * F;  // [k][k] WᵀW
-  double* sHH = sB + (size_t)k * k;  // [KP][KP]
-  double* sR = sHH + (size_t)KP * KP;  // [2][RED_NT]
+  double* sH = lds;                  // [k][F] new H
+  double* sH0 = sH + (size_t)k * F;  // [k][F] old H
+  double* sB = sH0 + (size_t)k * F;  // [k][k] WᵀW
+  double* sHH = sB + (size_t)k * k;  // [KP][KP] H·Hᵀ
+  double* sR = sHH + (size_t)KP * KP;  // [2][NWV]
 
   const bool have_ab = AB != nullptr;  // NULL when only deriving Ht/HHt from H64 (do_update=0)
+  for (int e = t; e < k * F; e += RED_NT) sH0[e] = H64[e];
   if (have_ab)
     for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
   __syncthreads();
   for (int e = t; e < k * F; e += RED_NT) {
     const int j = e / F;
     const int f = e - j * F;
-    double h = H64[e];
+    double h = sH0[e];
     if (do_update && have_ab) {
       const double num = AB[j * V + f];                       // (WᵀX)[j][f], SK:639
       double den = 0.0;                                       // ((WᵀW)·H)[j][f], SK:640
-      for (int m = 0; m < k; ++m) den = fma(sB[j * k + m], H64[m * F + f], den);
+      for (int m = 0; m < k; ++m) den = fma(sB[j * k + m], sH0[m * F + f], den);
       if (l1 > 0.0) den += l1;                                // SK:702-703
       if (l2 > 0.0) den = den + l2 * h;                       // SK:704-705
       if (den == 0.0) den = EPS32;                            // SK:706
@@ -559,33 +569,40 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
     const int j = e - f * KP;
     Ht[e] = j < k ? (TC)sH[j * F + f] : TC(0);
   }
-  for (int e = t; e < KP * KP; e += RED_NT) {
+  // HHt[j][m] = Σ_f H[j][f]·H[m][f]: one wave per entry, lanes over f, fixed-order shuffle tree
+  for (int e = wave; e < KP * KP; e += NWV) {
     const int j = e / KP;
     const int m = e - j * KP;
     double v = 0.0;
-    if (j < k && m < k)
-      for (int f = 0; f < F; ++f) v = fma(sH[j * F + f], sH[m * F + f], v);
-    sHH[e] = v;
-    HHt[e] = (TC)v;
+    if (j < k && m < k) {
+      for (int f = lane; f < F; f += 64) v = fma(sH[j * F + f], sH[m * F + f], v);
+      v = wave_sum(v);
+    }
+    if (lane == 0) {
+      sHH[e] = v;
+      HHt[e] = (TC)v;
+    }
   }
   if (stats && have_ab) {
     __syncthreads();
     double a = 0.0, b = 0.0;
     for (int e = t; e < k * F; e += RED_NT) a = fma(AB[(e / F) * V + (e % F)], sH[e], a);
     for (int e = t; e < k * k; e += RED_NT) b = fma(sB[e], sHH[(e / k) * KP + (e % k)], b);
-    sR[t] = a;
-    sR[RED_NT + t] = b;
-    __syncthreads();
-    for (int s = RED_NT / 2; s > 0; s >>= 1) {
-      if (t < s) {
-        sR[t] += sR[t + s];
-        sR[RED_NT + t] += sR[RED_NT + t + s];
-      }
-      __syncthreads();
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      sR[wave] = a;
+      sR[NWV + wave] = b;
     }
+    __syncthreads();
     if (t == 0) {
-      stats[0] = sR[0];
-      stats[1] = sR[RED_NT];
+      double sa = 0.0, sb = 0.0;
+      for (int w = 0; w < NWV; ++w) {
+        sa += sR[w];
+        sb += sR[NWV + w];
+      }
+      stats[0] = sa;
+      stats[1] = sb;
     }
   }
 }
@@ -604,7 +621,11 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
 
 // ------------------------------------------------------------------------------------------------
 // Deterministic fp64 reduction of partials[n_parts][n_out]; optional fused basis update.
-// grid = (ceil(n_out/64), nslice <= NSLICE); the ticket-elected last workgroup sums the stage rows.
+// grid = (ceil(n_out/64), nslice): block (c, s) sums rows of slice s for 64 outputs (<= 8 rows per
+// thread, one batch of independent loads) and writes one stage row write-through (sc1); one lane
+// per block then takes a ticket.  The block drawing the last ticket sums the stage rows with sc1
+// loads in a fixed order — the hand-off needs no release/acquire fence (MI355X_MICROARCH.md,
+// inter-workgroup visibility, "Valid forms" table row 1).
 // ------------------------------------------------------------------------------------------------
 struct UpdateArgs {
   double* H64;
@@ -615,6 +636,8 @@ struct UpdateArgs {
   double* stats;
   int tc_double;
 };
+
+constexpr int RED_ROWS_PER_THREAD = 8;
 
 __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict__ partials,
                                                         int64_t n_parts, int n_out, int nslice,
@@ -633,49 +656,44 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
   const int o = blockIdx.x * 64 + l;
   const int64_t lo = n_parts * blockIdx.y / nslice;
   const int64_t hi = n_parts * (blockIdx.y + 1) / nslice;
-  // rows lo+r, lo+r+4, ... : up to 8 independent loads in flight per thread, fixed summation order
   double s = 0.0;
   if (o < n_out) {
-    for (int64_t b0 = lo + r; b0 < hi; b0 += 32) {
-      double v[8];
+    double v[RED_ROWS_PER_THREAD];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int64_t b = b0 + 4 * u;
-        v[u] = b < hi ? partials[b * n_out + o] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
+    for (int u = 0; u < RED_ROWS_PER_THREAD; ++u) {
+      const int64_t b = lo + r + 4 * u;
+      v[u] = b < hi ? partials[b * n_out + o] : 0.0;
     }
+#pragma unroll
+    for (int u = 0; u < RED_ROWS_PER_THREAD; ++u) s += v[u];
   }
   red[t] = s;
   __syncthreads();
   if (r == 0 && o < n_out)
-    stage[(size_t)blockIdx.y * n_out + o] = ((red[l] + red[64 + l]) + red[128 + l]) + red[192 + l];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(stage + (size_t)blockIdx.y * n_out + o,
+                       ((red[l] + red[64 + l]) + red[128 + l]) + red[192 + l], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
   if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t total = gridDim.x * gridDim.y;
     const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == total - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
+    flag[0] = old == total - 1;
   }
   __syncthreads();
   if (!flag[0]) return;
   double* ab = fuse ? upd : nullptr;
   for (int oo = t; oo < n_out; oo += RED_NT) {
     double v = 0.0;
-    for (int s0 = 0; s0 < nslice; s0 += 8) {
-      double x[8];
+    for (int s0 = 0; s0 < nslice; s0 += 16) {
+      double x[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = s0 + u < nslice ? stage[(size_t)(s0 + u) * n_out + oo] : 0.0;
+      for (int u = 0; u < 16; ++u)
+        x[u] = s0 + u < nslice ? __hip_atomic_load(stage + (size_t)(s0 + u) * n_out + oo, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : 0.0;
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v += x[u];
+      for (int u = 0; u < 16; ++u) v += x[u];
     }
     out[oo] = v;
     if (fuse) ab[oo] = v;
@@ -908,7 +926,9 @@ static int launch_reduce(const double* partials, int64_t n_parts, int n_out, dou
   if (lds > 64 * 1024)
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&reduce_kernel),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int nslice = (int)std::max<int64_t>(1, std::min<int64_t>(NSLICE, (n_parts + 15) / 16));
+  const int nslice = (int)std::max<int64_t>(1, std::min<int64_t>(NSLICE, (n_parts + 4 * RED_ROWS_PER_THREAD - 1) / (4 * RED_ROWS_PER_THREAD)));
+  if ((int64_t)nslice * 4 * RED_ROWS_PER_THREAD < n_parts)
+    return set_err(CNMF_ERR_UNSUPPORTED, "too many partial rows (%lld) for one reduction", (long long)n_parts);
   dim3 grid((unsigned)((n_out + 63) / 64), (unsigned)nslice);
   hipLaunchKernelGGL(reduce_kernel, grid, dim3(RED_NT), lds, s, partials, n_parts, n_out, nslice,
                      stage, counter, out, fuse, ua);

@@ -145,7 +145,7 @@ class MUPlan:
                 check(self.lib.cnmf_mu_iterations(
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
-                    _ptr(self.counter), _ptr(self.AB), _ptr(self.stats), self.n_rows, self.F, self.k,
+                    _ptr(self.counter), _ptr(self.AB), None, self.n_rows, self.F, self.k,
                     self.l1_W, self.l2_W, self.l1_H, self.l2_H, _event_array(pass_events, n_iter),
                     self._stream()), "cnmf_mu_iterations")
             return

@@ -1,0 +1,50 @@
+"""Row-sharded MU across GPUs: one process per GPU, torch.distributed over RCCL.
+
+Each rank owns a contiguous block of rows of X and W; H is replicated.  Per iteration every rank runs
+the fused pass on its shard, reduces its per-workgroup partials to the k·(F+k) fp64 accumulators
+[WᵀX | WᵀW], ONE all_reduce(SUM) combines them over xGMI (backend "nccl" is RCCL on ROCm), and every
+rank applies the identical fp64 basis update — no broadcast.  The error check every 10 iterations
+all-reduces one double.  The sharding is exact: Σ_p W_pᵀX_p = WᵀX (tests/test_distributed.py).
+
+    import torch.distributed as dist
+    dist.init_process_group("nccl")
+    lo, hi = shard_bounds(n_rows, dist.get_world_size(), dist.get_rank())
+    W_r, H, n_iter = factorise_sharded(X[lo:hi], W0[lo:hi], H0, max_iter=500, tol=0)
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .solver import MUPlan, run_mu
+
+__all__ = ["shard_bounds", "factorise_sharded"]
+
+
+def shard_bounds(n_rows: int, world: int, rank: int):
+    """Contiguous, balanced [lo, hi) row range of `rank` (the first n_rows % world ranks get +1)."""
+    base, extra = divmod(int(n_rows), int(world))
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=0.0, l2_reg_W=0.0,
+                      l1_reg_H=0.0, l2_reg_H=0.0, update_H=True, group=None, device=None):
+    """MU on this rank's rows; returns (W_shard, H, n_iter) as device tensors.
+
+    X_shard: (n_r, F) float32/float64/bfloat16 tensor (any device; moved to `device`, default the
+    current HIP device), W_shard: (n_r, k), H0: (k, F) identical on every rank (broadcast from rank 0
+    here to make that true).  Regularisation constants are the already-scaled sklearn l1/l2 terms
+    (SK:1254-1265 computed on the GLOBAL n_samples).
+    """
+    if not (dist.is_available() and dist.is_initialized()):
+        raise RuntimeError("factorise_sharded needs an initialised torch.distributed process group")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    X = torch.as_tensor(X_shard).to(dev).contiguous()
+    H0 = torch.as_tensor(H0).to(dev, torch.float64).contiguous()
+    dist.broadcast(H0, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    plan = MUPlan(X, H0.shape[0], l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H, group=group)
+    plan.set_W(torch.as_tensor(W_shard))
+    plan.set_H(H0)
+    n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H)
+    return plan.W, plan.H(), n_iter

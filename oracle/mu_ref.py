@@ -146,3 +146,15 @@ def sharded_accumulators(X, W, n_shards):
         lo, hi = bounds[p], bounds[p + 1]
         out.append((W[lo:hi].T @ X[lo:hi], W[lo:hi].T @ W[lo:hi]))
     return out
+
+
+def update_h_from_accumulators(A, B, H, l1_reg_H=0.0, l2_reg_H=0.0):
+    """`update_h` (SK:634-728) expressed on the reduced accumulators A = WᵀX, B = WᵀW — the form the
+    sharded path applies after the all-reduce."""
+    denominator = B @ H
+    if l1_reg_H > 0:
+        denominator += l1_reg_H
+    if l2_reg_H > 0:
+        denominator = denominator + l2_reg_H * H
+    denominator[denominator == 0] = EPSILON
+    return H * (A / denominator)

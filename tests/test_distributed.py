@@ -1,0 +1,103 @@
+"""World-size-2 gloo test of the row-sharded MU orchestration on CPU.
+
+The multi-GPU host path (`MUPlan.iterate` / `run_mu` with world > 1: per-rank pass -> reduce ->
+all_reduce(AB) -> identical basis update; the loss check all-reduces one double) runs unchanged;
+only the three device launches are replaced by a NumPy stand-in (test-only: the product has no CPU
+path).  Two ranks on disjoint row shards must reproduce the unsharded oracle fit.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cnmf_amd import _lib
+from cnmf_amd.distributed import shard_bounds
+from cnmf_amd.solver import MUPlan, run_mu
+from oracle import mu_ref
+
+
+class _NumpyPlan(MUPlan):
+    """MUPlan with the three launches done by the oracle on CPU (fp64)."""
+
+    def __init__(self, X, W, H, group=None, regs=(0.0, 0.0, 0.0, 0.0)):  # noqa: D107 — no super()
+        self.X = np.asarray(X, dtype=np.float64)
+        self.n_rows, self.F = self.X.shape
+        self.k = H.shape[0]
+        self.V = self.F + self.k
+        self.n_out = self.k * self.V
+        self.l1_W, self.l2_W, self.l1_H, self.l2_H = regs
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.Wn = np.array(W, dtype=np.float64)
+        self.Hn = np.array(H, dtype=np.float64)
+        self.AB = torch.zeros(self.n_out, dtype=torch.float64)
+        self.loss_buf = torch.zeros(1, dtype=torch.float64)
+        self._partial = None
+
+    def sample_pass(self, flags):
+        if flags & _lib.PASS_LOSS:
+            R = self.X - self.Wn @ self.Hn
+            self._partial = np.array([np.sum(R * R)])
+            return
+        if flags & _lib.PASS_UPDATE_W:
+            self.Wn, _, _ = mu_ref.update_w(self.X, self.Wn, self.Hn, self.l1_W, self.l2_W)
+        if flags & _lib.PASS_ACCUMULATE:
+            A = self.Wn.T @ self.X
+            B = self.Wn.T @ self.Wn
+            self._partial = np.concatenate([A, B], axis=1).ravel()
+
+    def reduce(self, n_out, out):
+        out.copy_(torch.from_numpy(self._partial[:n_out]))
+
+    def basis_update(self):
+        AB = self.AB.numpy().reshape(self.k, self.V)
+        self.Hn = mu_ref.update_h_from_accumulators(AB[:, :self.F], AB[:, self.F:], self.Hn,
+                                                    self.l1_H, self.l2_H)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, X, W0, H0, max_iter, tol, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_bounds(X.shape[0], world, rank)
+        plan = _NumpyPlan(X[lo:hi], W0[lo:hi], H0)
+        n_iter = run_mu(plan, max_iter=max_iter, tol=tol)
+        out[rank] = (lo, hi, plan.Wn, plan.Hn, n_iter)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_bounds_cover_rows():
+    for n, w in [(10, 3), (1_000_000, 8), (7, 8), (0, 2)]:
+        b = [shard_bounds(n, w, r) for r in range(w)]
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+        assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
+
+
+@pytest.mark.parametrize("tol,max_iter", [(0.0, 30), (1e-3, 400)])
+def test_two_rank_gloo_matches_unsharded(tol, max_iter):
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(301, 81, seed=11, dtype=np.float64)
+    W0, H0 = random_init(X, 4, 3)
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_worker, args=(2, _free_port(), X, W0, H0, max_iter, tol, out), nprocs=2, join=True)
+    Wr, Hr, nr = mu_ref.mu_fit(X, W0, H0, max_iter=max_iter, tol=tol)
+    W = np.zeros_like(W0)
+    for rank in range(2):
+        lo, hi, Wp, Hp, n_iter = out[rank]
+        W[lo:hi] = Wp
+        assert n_iter == nr
+        np.testing.assert_allclose(Hp, Hr, rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(W, Wr, rtol=1e-10, atol=1e-14)

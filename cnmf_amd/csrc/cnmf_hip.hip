@@ -104,7 +104,6 @@ struct PassLds {
   size_t region0;  // X tile [TS][F] (+4 zero elements), later the cross-wave reduction scratch
   size_t w;        // old-W tile, flat [ns][k]
   size_t wn;       // new-W tile, [TS][KP] (zero for j >= k and for invalid samples)
-  size_t p;        // partial num, [NWAVE][TS][KP]
   size_t ht;       // Ht, [4*q][KP], rows >= F zero (q = ceil(F/4): each wave owns q features)
   size_t hht;      // HHt, [KP][KP]
   size_t zero;     // 16 zero bytes (source of the idle lanes of the A phase)
@@ -120,8 +119,7 @@ __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc)
   L.region0 = xb > rb ? xb : rb;
   L.w = L.region0;
   L.wn = L.w + align16((size_t)TS * KP * sc);
-  L.p = L.wn + align16((size_t)TS * KP * sc);
-  L.ht = L.p + align16((size_t)NWAVE * TS * KP * sc);
+  L.ht = L.wn + align16((size_t)TS * KP * sc);
   L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sc);
   L.zero = L.hht + align16((size_t)KP * KP * sc);
   L.total = L.zero + 16;
@@ -223,7 +221,6 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  TC* sP = reinterpret_cast<TC*>(smem + L.p);
   TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
   TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
@@ -300,15 +297,21 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
       }
     }
 
-    // ---- phase 1: lane = sample, wave = quarter of the (zero-padded) features
+    // ---- phases 1+2, wave-local: wave w owns samples [16w, 16w+16); lane = (sample s = lane/4,
+    //      feature quarter qtr = lane%4).  Each lane sums its quarter of x[s]·Ht (Ht rows >= F
+    //      are zero), a quad shuffle (fixed order (q0+q1)+(q2+q3)) completes num[s][0..KP), then
+    //      lane (s, qtr) updates components j = qtr + 4c.  No block barrier, no LDS exchange.
+    const int s_beg = wave * (TS / NWAVE);
     {
-      const int fb = wave * q;
-      const TX* xr = sX + (size_t)lane * F + fb;
+      const int qtr = lane & 3;
+      const int s = s_beg + (lane >> 2);
+      const int fb = qtr * q;
+      const TX* xr = sX + (size_t)s * F + fb;
       const TC* hb = sHt + (size_t)fb * KP;
       if (do_loss) {
         TC w[KP];
 #pragma unroll
-        for (int j = 0; j < KP; ++j) w[j] = (j < k && lane < ns) ? sW[lane * k + j] : TC(0);
+        for (int j = 0; j < KP; ++j) w[j] = (j < k && s < ns) ? sW[s * k + j] : TC(0);
         const int nf = min(q, F - fb);
         TC part = 0;
         for (int f = 0; f < nf; ++f) {
@@ -319,7 +322,9 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
           const TC r = xv - wh;
           part = fma(r, r, part);
         }
-        if (lane < ns) loss64 += (double)part;
+        part += __shfl_xor(part, 1);
+        part += __shfl_xor(part, 2);
+        if (qtr == 0 && s < ns) loss64 += (double)part;
       } else {
         TC p[KP];
 #pragma unroll
@@ -341,54 +346,46 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
           }
         }
 #pragma unroll
-        for (int j = 0; j < KP; ++j) sP[(wave * TS + lane) * KP + j] = p[j];
-      }
-    }
-    __syncthreads();
-
-    if (do_upd) {
-      // ---- phase 2: element (s, j) = flat index e of the [TS][KP] tile; W <- W·(num/den)
-#pragma unroll
-      for (int c = 0; c < KP / 4; ++c) {
-        const int e = t + NT * c;
-        const int s = e / KP;
-        const int j = e % KP;
-        TC wn = 0;
-        if (s < ns && j < k) {
-          const TC num = ((sP[(0 * TS + s) * KP + j] + sP[(1 * TS + s) * KP + j]) +
-                          sP[(2 * TS + s) * KP + j]) + sP[(3 * TS + s) * KP + j];
-          TC den = 0;
-          TC wold;
-          if (k == KP) {
-            TC wr[KP];
-#pragma unroll
-            for (int m = 0; m < KP; ++m) wr[m] = sW[s * KP + m];
-#pragma unroll
-            for (int m = 0; m < KP; ++m) den = fma(wr[m], sHHt[m * KP + j], den);
-            wold = sW[s * KP + j];
-          } else {
-#pragma unroll
-            for (int m = 0; m < KP; ++m)
-              if (m < k) den = fma(sW[s * k + m], sHHt[m * KP + j], den);
-            wold = sW[s * k + j];
-          }
-          if (l1 > TC(0)) den += l1;                    // SK:616-617
-          if (l2 > TC(0)) den = den + l2 * wold;        // SK:618-619
-          if (den == TC(0)) den = TC(EPS32);            // SK:620
-          const TC qv = num / den;                      // SK:622
-          wn = wold * qv;                               // SK:629
-          W[(size_t)(tile * TS + s) * k + j] = wn;
+        for (int j = 0; j < KP; ++j) {
+          p[j] += __shfl_xor(p[j], 1);
+          p[j] += __shfl_xor(p[j], 2);
         }
-        sWn[s * KP + j] = wn;
+        if (do_upd) {
+          TC wr[KP];
+#pragma unroll
+          for (int m = 0; m < KP; ++m)
+            wr[m] = (k == KP) ? sW[s * KP + m] : ((m < k) ? sW[s * k + m] : TC(0));
+#pragma unroll
+          for (int c = 0; c < KP / 4; ++c) {
+            const int j = qtr + 4 * c;
+            const TC num = qtr == 0 ? p[4 * c] : (qtr == 1 ? p[4 * c + 1] : (qtr == 2 ? p[4 * c + 2] : p[4 * c + 3]));
+            const TC wold = qtr == 0 ? wr[4 * c] : (qtr == 1 ? wr[4 * c + 1] : (qtr == 2 ? wr[4 * c + 2] : wr[4 * c + 3]));
+            TC wn = 0;
+            if (s < ns && j < k) {
+              TC den = 0;
+#pragma unroll
+              for (int m = 0; m < KP; ++m) den = fma(wr[m], sHHt[j * KP + m], den);  // HHt symmetric
+              if (l1 > TC(0)) den += l1;                    // SK:616-617
+              if (l2 > TC(0)) den = den + l2 * wold;        // SK:618-619
+              if (den == TC(0)) den = TC(EPS32);            // SK:620
+              const TC qv = num / den;                      // SK:622
+              wn = wold * qv;                               // SK:629
+              W[(size_t)(tile * TS + s) * k + j] = wn;
+            }
+            sWn[s * KP + j] = wn;
+          }
+          if (SPLIT)
+            __builtin_amdgcn_wave_barrier();  // sWn rows of this wave feed its own A phase
+          else
+            __syncthreads();                  // wide rows: the A phase reads every wave's rows
+        }
       }
-      __syncthreads();
     }
 
     if (do_acc) {
       // ---- phase 3: lane = virtual feature v (v < F: X column, F <= v < F+k: W_new column,
       //      beyond: a zero word); acc[j][v] += w_new[s][j]·value[s][v]  (SK:639-640)
       if (SPLIT) {
-        const int s_beg = wave * (TS / NWAVE);
         const int nsw = min(max(ns - s_beg, 0), TS / NWAVE);
         // per-lane byte offset / stride of each pass's source column
         uint32_t offx[NPW], stx[NPW], offw[NPW], stw[NPW];

@@ -35,6 +35,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <unordered_map>
@@ -172,6 +173,40 @@ __device__ __forceinline__ void prefetch_tile(u32x4 (&pf)[N], const TileGeom& g,
   }
 }
 
+// Write one staged tile into LDS: the prefetched registers, any chunks beyond the register depth,
+// and for a ragged last tile the element tails plus 4 zero elements after the last valid row (the
+// padded feature reads of phase 1 multiply them by zero Ht rows, so they must not hold NaN bits).
+template <typename TX, typename TC, int N>
+__device__ __forceinline__ void stage_tile(unsigned char* smem, size_t w_off, const TileGeom& g,
+                                           const u32x4 (&pf)[N], int t, int F) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int c = t + NT * i;
+    if (c < g.nch) {
+      unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + w_off + 16 * (size_t)(c - g.nxf);
+      *reinterpret_cast<u32x4*>(dst) = pf[i];
+    }
+  }
+  for (int c = t + NT * N; c < g.nch; c += NT) {
+    const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
+    unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + w_off + 16 * (size_t)(c - g.nxf);
+    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
+  }
+  if (g.ns < TS) {
+    TX* sX = reinterpret_cast<TX*>(smem);
+    TC* sW = reinterpret_cast<TC*>(smem + w_off);
+    if (t < g.rx) {
+      const int e = g.nxf * (16 / (int)sizeof(TX)) + t;
+      sX[e] = reinterpret_cast<const TX*>(g.xsrc)[e];
+    }
+    if (t >= 64 && t - 64 < g.rw) {
+      const int e = g.nwf * (16 / (int)sizeof(TC)) + (t - 64);
+      sW[e] = reinterpret_cast<const TC*>(g.wsrc)[e];
+    }
+    if (t >= 128 && t - 128 < 4) sX[g.ns * F + (t - 128)] = TX{};
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
   return *reinterpret_cast<const T*>(smem + off);
@@ -261,32 +296,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   for (; tile < n_tiles; tile += gridDim.x) {
     const TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
     const int ns = g.ns;
-    // ---- stage tile `tile` (prefetched registers + any overflow chunks + ragged tail) into LDS
-#pragma unroll
-    for (int i = 0; i < PFT; ++i) {
-      int c = t + NT * i;
-      if (c < g.nch) {
-        unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
-        *reinterpret_cast<u32x4*>(dst) = pf[i];
-      }
-    }
-    for (int c = t + NT * PFT; c < g.nch; c += NT) {
-      const unsigned char* src = c < g.nxf ? g.xsrc + 16 * (size_t)c : g.wsrc + 16 * (size_t)(c - g.nxf);
-      unsigned char* dst = c < g.nxf ? smem + 16 * (size_t)c : smem + L.w + 16 * (size_t)(c - g.nxf);
-      *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(src);
-    }
-    if (ns < TS) {  // ragged last tile: element tails, and zeros after the last valid row so the
-                    // padded feature reads of phase 1 (Ht rows >= F are zero) never meet NaN bits
-      if (t < g.rx) {
-        int e = g.nxf * (16 / (int)sizeof(TX)) + t;
-        sX[e] = reinterpret_cast<const TX*>(g.xsrc)[e];
-      }
-      if (t >= 64 && t - 64 < g.rw) {
-        int e = g.nwf * (16 / (int)sizeof(TC)) + (t - 64);
-        sW[e] = reinterpret_cast<const TC*>(g.wsrc)[e];
-      }
-      if (t >= 128 && t - 128 < 4) sX[ns * F + (t - 128)] = TX{};
-    }
+    stage_tile<TX, TC, PFT>(smem, L.w, g, pf, t, F);
     __syncthreads();
 
     // ---- issue the next tile's loads; they stay in flight through this tile's compute
@@ -508,6 +518,212 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
     if (lane == 0) sRed[wave] = loss64;
     __syncthreads();
     if (t == 0) partials[blockIdx.x] = ((sRed[0] + sRed[1]) + sRed[2]) + sRed[3];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The fused sample pass on the matrix cores (fp32 compute; X fp32 or bf16; V = F + k <= 128).
+//
+// Same tile pipeline as mu_pass_kernel (64-sample tiles, register prefetch one tile ahead, 2
+// barriers per tile); each wave owns 16 samples and runs its two small GEMMs on
+// v_mfma_f32_16x16x4_f32 (exact fp32: a k-ordered fmaf chain, MI355X_MICROARCH.md §Matrix cores):
+//   phase 1  num[j][s]  = Σ_f Ht[f][j]·x[s][f]      M = j (16, KP used), N = 16 samples,
+//                                                    K = F in steps of 4; the Ht operand lives in
+//                                                    VGPRs for the whole launch
+//   phase 2  lane (s, j-group) applies the MU update to 4 components (W <- W·num/den)
+//   phase 3  acc[j][v] += Σ_s w'[s][j]·[x | w'][s][v] M = j, N = V in 16-column blocks,
+//                                                    K = the wave's 16 samples
+// The accumulators stay in registers for the whole launch; the 4 waves are combined in fp64 at
+// the end exactly like mu_pass_kernel (same partial-row layout [k][F+k]).
+// ------------------------------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int NB_MAX = 8;  // 16-column blocks of [X | W'] (V <= 128)
+
+template <typename TX, int KP, int FT>
+__global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 3 : 4) : 2) void mu_pass_mfma_kernel(const TX* __restrict__ X,
+                                                            float* __restrict__ W,
+                                                            const float* __restrict__ Ht,
+                                                            const float* __restrict__ HHt,
+                                                            double* __restrict__ partials,
+                                                            int64_t n_rows, int F_rt, int k, float l1,
+                                                            float l2, int flags, int64_t n_tiles) {
+  using TC = float;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int F = FT > 0 ? FT : F_rt;
+  const int nk1 = (F + 3) >> 2;        // phase-1 K-steps
+  const int V = F + k;
+  const int nb_cnt = (V + 15) >> 4;    // phase-3 column blocks
+  const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC));
+  TX* sX = reinterpret_cast<TX*>(smem);
+  TC* sW = reinterpret_cast<TC*>(smem + L.w);
+  TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
+  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
+  TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
+  double* sRed = reinterpret_cast<double*>(smem);
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int ln = lane & 15;  // MFMA row/column index of this lane
+  const int lk = lane >> 4;  // MFMA k index of this lane (and C/D row group)
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int s_beg = wave * (TS / NWAVE);
+  const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+
+  for (int e = t; e < NWAVE * feat_per_wave(F) * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : TC(0);
+  for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
+  if (t < 4) {
+    sX[TS * F + t] = TX{};
+    reinterpret_cast<uint32_t*>(smem + L.zero)[t] = 0u;
+  }
+  // phase-1 A operand Ht[4s+lk][ln]: held in VGPRs when the prefetch buffer leaves room for it
+  // (bf16 X), else read from the LDS copy of Ht each K-step
+  constexpr int NK1C = FT > 0 ? (FT + 3) / 4 : 1;
+  constexpr bool A1_REG = FT > 0 && sizeof(TX) == 2 && KP == 4;
+  float a1[A1_REG ? NK1C : 1];
+  if constexpr (A1_REG) {
+#pragma unroll
+    for (int st = 0; st < NK1C; ++st) {
+      const int f = 4 * st + lk;
+      a1[st] = (f < F && ln < KP) ? Ht[f * KP + ln] : 0.0f;
+    }
+  }
+
+  // column blocks held in registers: exact for a compile-time F (k <= KP), NB_MAX otherwise
+  constexpr int NBC = FT > 0 ? (FT + KP + 15) / 16 : NB_MAX;
+  f32x4 acc[NBC];
+#pragma unroll
+  for (int nb = 0; nb < NBC; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int PFT = FT > 0 ? (int)((TS * FT * sizeof(TX) + TS * KP * sizeof(TC) + 16 * NT - 1) / (16 * NT)) : PF;
+  u32x4 pf[PFT];
+  int64_t tile = blockIdx.x;
+  if (tile < n_tiles) prefetch_tile<PFT>(pf, tile_geom(X, W, tile, n_rows, F, k), t);
+
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
+    const int ns = g.ns;
+    stage_tile<TX, TC, PFT>(smem, L.w, g, pf, t, F);
+    __syncthreads();
+    {
+      const int64_t nt = tile + gridDim.x;
+      if (nt < n_tiles) prefetch_tile<PFT>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
+    }
+
+    // ---- phase 1: d1[r] = num[s = s_beg + ln][j = 4*lk + r]
+    const int s = s_beg + ln;
+    f32x4 d1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      const TX* xb = sX + (size_t)s * F + lk;
+      if constexpr (A1_REG) {
+#pragma unroll 7
+        for (int st = 0; st < NK1C; ++st)
+          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], to_c(xb[4 * st]), d1, 0, 0, 0);
+      } else if constexpr (FT > 0) {
+        const float* hb = sHt + lk * KP + ln;  // Ht[4st+lk][ln]; rows >= F and columns >= k are 0
+#pragma unroll 7
+        for (int st = 0; st < NK1C; ++st) {
+          const float a = ln < KP ? hb[4 * st * KP] : 0.0f;
+          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, to_c(xb[4 * st]), d1, 0, 0, 0);
+        }
+      } else {
+        for (int st = 0; st < nk1; ++st) {
+          const int f = 4 * st + lk;
+          const float a = (f < F && ln < KP) ? sHt[f * KP + ln] : 0.0f;
+          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, to_c(xb[4 * st]), d1, 0, 0, 0);
+        }
+      }
+    }
+
+    if (do_upd) {
+      // ---- phase 2: lanes with 4*lk < KP update components j = 4*lk + r of sample s
+      if (4 * lk < KP) {
+        float wr[KP];
+#pragma unroll
+        for (int m = 0; m < KP; ++m)
+          wr[m] = (k == KP) ? sW[s * KP + m] : ((m < k) ? sW[s * k + m] : 0.0f);
+        float wn[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int j = 4 * lk + r;
+          float wold = 0.0f;
+#pragma unroll
+          for (int m = 0; m < KP; ++m)
+            if (m == j) wold = wr[m];
+          float den = 0.0f;
+#pragma unroll
+          for (int m = 0; m < KP; ++m) den = fmaf(wr[m], sHHt[j * KP + m], den);  // HHt symmetric
+          if (l1 > 0.0f) den += l1;                    // SK:616-617
+          if (l2 > 0.0f) den = den + l2 * wold;        // SK:618-619
+          if (den == 0.0f) den = (float)EPS32;         // SK:620
+          const float qv = d1[r] / den;                // SK:622
+          wn[r] = (s < ns && j < k) ? wold * qv : 0.0f;  // SK:629
+          sWn[s * KP + j] = wn[r];
+        }
+        if (s < ns) {
+          float* wrow = W + (size_t)(tile * TS + s) * k + 4 * lk;
+          if (k == KP) {
+            *reinterpret_cast<f32x4*>(wrow) = f32x4{wn[0], wn[1], wn[2], wn[3]};
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (4 * lk + r < k) wrow[r] = wn[r];
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();  // this wave's sWn rows feed its own phase 3
+    }
+
+    if (do_acc) {
+      // ---- phase 3: acc[nb][r] = Σ_s w'[s][4lk+r]·val[s][16nb+ln]
+#pragma unroll 2
+      for (int st = 0; st < TS / NWAVE / 4; ++st) {
+        const int ss = s_beg + 4 * st + lk;
+        const bool sv = ss < ns;
+        const float a3 = ln < KP ? sWn[ss * KP + min(ln, KP - 1)] : 0.0f;
+#pragma unroll
+        for (int nb = 0; nb < NBC; ++nb) {
+          if (nb < nb_cnt) {
+            const int v = 16 * nb + ln;
+            float b3;
+            if (16 * nb + 16 <= F) {
+              b3 = to_c(sX[(size_t)ss * F + v]);
+            } else {
+              const float vx = to_c(sX[(size_t)ss * F + min(v, F - 1)]);
+              const float vw = sWn[ss * KP + min(max(v - F, 0), KP - 1)];
+              b3 = v < F ? vx : (v < V ? vw : 0.0f);
+            }
+            b3 = sv ? b3 : 0.0f;
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a3, b3, acc[nb], 0, 0, 0);
+          }
+        }
+      }
+    }
+    __syncthreads();  // LDS tiles are rewritten by the next iteration
+  }
+
+  // ---- per-workgroup partial rows: D3[j = 4lk + r][v = 16nb + ln], 4 waves summed in fp64
+  if (do_acc) {
+    const int n_out = k * V;
+    double* prow = partials + (size_t)blockIdx.x * n_out;
+#pragma unroll
+    for (int nb = 0; nb < NBC; ++nb) {
+      if (nb < nb_cnt) {
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sRed[(wave * 64 + lane) * 4 + r] = (double)acc[nb][r];
+        __syncthreads();
+        const int l = t & 63;
+        const int r = t >> 6;
+        const int j = 4 * (l >> 4) + r;
+        const int v = 16 * nb + (l & 15);
+        if (j < k && v < V) {
+          const double sum = ((sRed[(0 * 64 + l) * 4 + r] + sRed[(1 * 64 + l) * 4 + r]) +
+                              sRed[(2 * 64 + l) * 4 + r]) + sRed[(3 * 64 + l) * 4 + r];
+          prow[j * V + v] = sum;
+        }
+      }
+    }
   }
 }
 
@@ -777,17 +993,37 @@ static bool pick_tx(int KP, int F, int np, PassKernel* out) {
   return false;
 }
 
+template <typename TX, int KP>
+static PassKernel make_mfma(int F) {
+  PassFn fn = F == 81 ? reinterpret_cast<PassFn>(&mu_pass_mfma_kernel<TX, KP, 81>)
+                      : reinterpret_cast<PassFn>(&mu_pass_mfma_kernel<TX, KP, 0>);
+  return PassKernel{fn, KP, 0, true, sizeof(TX), sizeof(float)};
+}
+
+// The matrix-core pass serves fp32 / bf16 X whose [X | W] rows fit 8 column blocks (V <= 128).
+static bool pick_mfma(int x_dtype, int F, int k, PassKernel* out) {
+  if (F + k > 16 * NB_MAX || (x_dtype != CNMF_F32 && x_dtype != CNMF_BF16)) return false;
+  const int KP = k <= 4 ? 4 : (k <= 8 ? 8 : 16);
+  const bool bf = x_dtype == CNMF_BF16;
+  switch (KP) {
+    case 4: *out = bf ? make_mfma<bf16_t, 4>(F) : make_mfma<float, 4>(F); return true;
+    case 8: *out = bf ? make_mfma<bf16_t, 8>(F) : make_mfma<float, 8>(F); return true;
+    default: *out = bf ? make_mfma<bf16_t, 16>(F) : make_mfma<float, 16>(F); return true;
+  }
+}
+
 static int padded_k(int k) { return k <= 4 ? 4 : (k <= 8 ? 8 : 16); }
 
 static constexpr size_t kMaxLds = 160 * 1024;
+static bool g_force_valu = getenv("CNMF_FORCE_VALU") != nullptr;  // A/B switch for benchmarking
 
-static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds) {
+static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds, bool mfma_ok = true) {
   if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
   if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
   const int KP = padded_k(k);
   const int np = (F + k + 63) / 64;
-  bool ok = false;
-  switch (x_dtype) {
+  bool ok = mfma_ok && !g_force_valu && pick_mfma(x_dtype, F, k, pk);
+  if (!ok) switch (x_dtype) {
     case CNMF_F32: ok = pick_tx<float>(KP, F, np, pk); break;
     case CNMF_F64: ok = pick_tx<double>(KP, F, np, pk); break;
     case CNMF_BF16: ok = pick_tx<bf16_t>(KP, F, np, pk); break;
@@ -891,13 +1127,22 @@ int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, con
     return set_err(CNMF_ERR_ARG, "partials required");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
-  PassKernel pk;
-  size_t lds = 0;
-  int st = select_pass(x_dtype, n_features, k, &pk, &lds);
+  // every launch of a shape uses the grid of its main (accumulating) kernel, so the number of
+  // partial rows is one per shape (cnmf_pass_blocks) whatever the flags
+  PassKernel pmain;
+  size_t lmain = 0;
+  int st = select_pass(x_dtype, n_features, k, &pmain, &lmain);
   if (st) return st;
-  const int64_t nb = pass_grid(n_rows, pk.fn, lds);
+  const int64_t nb = pass_grid(n_rows, pmain.fn, lmain);
   if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (nb == 0) return CNMF_OK;
+  PassKernel pk = pmain;
+  size_t lds = lmain;
+  if (flags & CNMF_PASS_LOSS) {
+    st = select_pass(x_dtype, n_features, k, &pk, &lds, false);
+    if (st) return st;
+    if (max_resident(pk.fn, lds) <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  }
   const int64_t n_tiles = (n_rows + TS - 1) / TS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int F = n_features;

@@ -51,9 +51,9 @@ _SIGS = {
     "cnmf_mu_sample_pass": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f64, _f64,
                                    _i32, _vp]),
     "cnmf_reduce_partials": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _vp]),
-    "cnmf_basis_update": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _i32, _f64, _f64, _i32, _vp, _vp]),
-    "cnmf_reduce_update": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _f64,
-                                  _f64, _vp, _vp]),
+    "cnmf_basis_update": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64, _i32, _vp, _vp]),
+    "cnmf_reduce_update": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64,
+                                  _vp, _vp]),
     "cnmf_hbm_probe": (_i32, [_vp, _i64, _vp, _i32, _vp]),
     "cnmf_mu_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                   _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp]),

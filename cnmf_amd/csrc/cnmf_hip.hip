@@ -105,8 +105,8 @@ struct PassLds {
   size_t region0;  // X tile [TS][F] (+4 zero elements), later the cross-wave reduction scratch
   size_t w;        // old-W tile, flat [ns][k]
   size_t wn;       // new-W tile, [TS][KP] (zero for j >= k and for invalid samples)
-  size_t ht;       // Ht, [4*q][KP], rows >= F zero (q = ceil(F/4): each wave owns q features)
-  size_t hht;      // HHt, [KP][KP]
+  size_t ht;       // Ht (fp64), [4*q][KP], rows >= F zero (q = ceil(F/4): a lane sums q features)
+  size_t hht;      // HHt (fp64), [KP][KP]
   size_t zero;     // 16 zero bytes (source of the idle lanes of the A phase)
   size_t total;
 };
@@ -121,8 +121,8 @@ __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc)
   L.w = L.region0;
   L.wn = L.w + align16((size_t)TS * KP * sc);
   L.ht = L.wn + align16((size_t)TS * KP * sc);
-  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sc);
-  L.zero = L.hht + align16((size_t)KP * KP * sc);
+  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sizeof(double));
+  L.zero = L.hht + align16((size_t)KP * KP * sizeof(double));
   L.total = L.zero + 16;
   return L;
 }
@@ -212,6 +212,102 @@ __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
   return *reinterpret_cast<const T*>(smem + off);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Phases 1+2 of a tile, shared by both pass kernels; wave-local (wave w owns samples
+// [16w, 16w+16), lane = (sample s = lane/4, feature quarter qtr = lane%4)) and in fp64.
+//
+// Why fp64: the 81-term dot products num = x·Hᵀ summed in fp32 leave a rounding error that is
+// nearly the SAME every iteration once H settles, so it drifts coherently instead of averaging out:
+// 500 iterations of k=8 MU end 1.8e-5 (rel. Frobenius) from the fp64 oracle with fp32 sums and
+// 6e-7 with fp64 sums (NumPy emulation of this kernel's arithmetic).  An fp32
+// product is exact in fp64, so each step is one v_fma_f64 on the converted x.
+//   phase 1: lane sums its quarter of x[s]·Ht (Ht rows >= F are zero), quad shuffles in the fixed
+//            order (q0+q1)+(q2+q3) complete num[s][0..KP) in every lane of the quad;
+//   phase 2: lane (s, qtr) updates components j = qtr + 4c:
+//            den = Σ_m w[s][m]·HHt[j][m] (+l1)(+l2·w), den==0 -> eps32, w' = w·(num/den) in fp64,
+//            rounded once to TC, stored to HBM and to the LDS row sWn[s] (A phase input).
+//   loss   : lane sums (x − w·Ht)² over its quarter, quad-reduced into loss64 (qtr 0 lanes).
+// ------------------------------------------------------------------------------------------------
+template <typename TX, typename TC, int KP, int FT>
+__device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __restrict__ sW,
+                                        TC* __restrict__ sWn, const double* __restrict__ sHt,
+                                        const double* __restrict__ sHHt, TC* __restrict__ W,
+                                        int64_t tile, int F, int q, int k, int ns, int s_beg,
+                                        int lane, bool do_loss, bool do_upd, double l1, double l2,
+                                        double& loss64) {
+  const int qtr = lane & 3;
+  const int s = s_beg + (lane >> 2);
+  const int fb = qtr * q;
+  const TX* xr = sX + (size_t)s * F + fb;
+  const double* hb = sHt + (size_t)fb * KP;
+  if (do_loss) {
+    double w[KP];
+#pragma unroll
+    for (int j = 0; j < KP; ++j) w[j] = (j < k && s < ns) ? (double)sW[s * k + j] : 0.0;
+    const int nf = min(q, F - fb);
+    double part = 0.0;
+    for (int f = 0; f < nf; ++f) {
+      double wh = 0.0;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) wh = fma(w[j], hb[f * KP + j], wh);
+      const double r = (double)to_c(xr[f]) - wh;
+      part = fma(r, r, part);
+    }
+    part += __shfl_xor(part, 1);
+    part += __shfl_xor(part, 2);
+    if (qtr == 0 && s < ns) loss64 += part;
+    return;
+  }
+  double p[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) p[j] = 0.0;
+  if constexpr (FT > 0) {
+    constexpr int QF = (FT + NWAVE - 1) / NWAVE;
+#pragma unroll 2
+    for (int f = 0; f < QF; ++f) {
+      const double xv = (double)to_c(xr[f]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+    }
+  } else {
+#pragma unroll 4
+    for (int f = 0; f < q; ++f) {
+      const double xv = (double)to_c(xr[f]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    p[j] += __shfl_xor(p[j], 1);
+    p[j] += __shfl_xor(p[j], 2);
+  }
+  if (!do_upd) return;
+  double wr[KP];
+#pragma unroll
+  for (int m = 0; m < KP; ++m)
+    wr[m] = (k == KP) ? (double)sW[s * KP + m] : ((m < k) ? (double)sW[s * k + m] : 0.0);
+#pragma unroll
+  for (int c = 0; c < KP / 4; ++c) {
+    const int j = qtr + 4 * c;
+    const double num = qtr == 0 ? p[4 * c] : (qtr == 1 ? p[4 * c + 1] : (qtr == 2 ? p[4 * c + 2] : p[4 * c + 3]));
+    const double wold = qtr == 0 ? wr[4 * c] : (qtr == 1 ? wr[4 * c + 1] : (qtr == 2 ? wr[4 * c + 2] : wr[4 * c + 3]));
+    TC wn = TC(0);
+    if (s < ns && j < k) {
+      double den = 0.0;
+#pragma unroll
+      for (int m = 0; m < KP; ++m) den = fma(wr[m], sHHt[j * KP + m], den);  // HHt symmetric
+      if (l1 > 0.0) den += l1;                    // SK:616-617
+      if (l2 > 0.0) den = den + l2 * wold;        // SK:618-619
+      if (den == 0.0) den = EPS32;                // SK:620
+      wn = (TC)(wold * (num / den));              // SK:622-629
+      W[(size_t)(tile * TS + s) * k + j] = wn;
+    }
+    sWn[s * KP + j] = wn;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // The fused sample pass.
 //   TX: X storage (float / double / bf16_t), TC: compute + W type, KP: padded k (4/8/16),
@@ -241,12 +337,11 @@ constexpr int pass_min_waves() {
 template <typename TX, int KP, int FT, int NPW, bool SPLIT>
 __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_kernel(const TX* __restrict__ X,
                                                      typename Compute<TX>::T* __restrict__ W,
-                                                     const typename Compute<TX>::T* __restrict__ Ht,
-                                                     const typename Compute<TX>::T* __restrict__ HHt,
+                                                     const double* __restrict__ Ht,
+                                                     const double* __restrict__ HHt,
                                                      double* __restrict__ partials, int64_t n_rows,
-                                                     int F_rt, int k, typename Compute<TX>::T l1,
-                                                     typename Compute<TX>::T l2, int flags,
-                                                     int64_t n_tiles) {
+                                                     int F_rt, int k, double l1, double l2,
+                                                     int flags, int64_t n_tiles) {
   using TC = typename Compute<TX>::T;
   constexpr bool SAME = sizeof(TX) == sizeof(TC);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -256,8 +351,8 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
-  TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
+  double* sHt = reinterpret_cast<double*>(smem + L.ht);
+  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
   const int t = threadIdx.x;
@@ -270,7 +365,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
 
   // basis-side constants into LDS once per launch (Ht zero-padded to 4q rows)
-  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : TC(0);
+  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : 0.0;
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
   if (t < 4) {
     sX[TS * F + t] = TX{};
@@ -307,89 +402,15 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
       }
     }
 
-    // ---- phases 1+2, wave-local: wave w owns samples [16w, 16w+16); lane = (sample s = lane/4,
-    //      feature quarter qtr = lane%4).  Each lane sums its quarter of x[s]·Ht (Ht rows >= F
-    //      are zero), a quad shuffle (fixed order (q0+q1)+(q2+q3)) completes num[s][0..KP), then
-    //      lane (s, qtr) updates components j = qtr + 4c.  No block barrier, no LDS exchange.
+    // ---- phases 1+2 (wave-local, fp64)
     const int s_beg = wave * (TS / NWAVE);
-    {
-      const int qtr = lane & 3;
-      const int s = s_beg + (lane >> 2);
-      const int fb = qtr * q;
-      const TX* xr = sX + (size_t)s * F + fb;
-      const TC* hb = sHt + (size_t)fb * KP;
-      if (do_loss) {
-        TC w[KP];
-#pragma unroll
-        for (int j = 0; j < KP; ++j) w[j] = (j < k && s < ns) ? sW[s * k + j] : TC(0);
-        const int nf = min(q, F - fb);
-        TC part = 0;
-        for (int f = 0; f < nf; ++f) {
-          const TC xv = to_c(xr[f]);
-          TC wh = 0;
-#pragma unroll
-          for (int j = 0; j < KP; ++j) wh = fma(w[j], hb[f * KP + j], wh);
-          const TC r = xv - wh;
-          part = fma(r, r, part);
-        }
-        part += __shfl_xor(part, 1);
-        part += __shfl_xor(part, 2);
-        if (qtr == 0 && s < ns) loss64 += (double)part;
-      } else {
-        TC p[KP];
-#pragma unroll
-        for (int j = 0; j < KP; ++j) p[j] = 0;
-        if constexpr (FT > 0) {
-          constexpr int QF = (FT + NWAVE - 1) / NWAVE;
-#pragma unroll 7
-          for (int f = 0; f < QF; ++f) {
-            const TC xv = to_c(xr[f]);
-#pragma unroll
-            for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
-          }
-        } else {
-#pragma unroll 4
-          for (int f = 0; f < q; ++f) {
-            const TC xv = to_c(xr[f]);
-#pragma unroll
-            for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < KP; ++j) {
-          p[j] += __shfl_xor(p[j], 1);
-          p[j] += __shfl_xor(p[j], 2);
-        }
-        if (do_upd) {
-          TC wr[KP];
-#pragma unroll
-          for (int m = 0; m < KP; ++m)
-            wr[m] = (k == KP) ? sW[s * KP + m] : ((m < k) ? sW[s * k + m] : TC(0));
-#pragma unroll
-          for (int c = 0; c < KP / 4; ++c) {
-            const int j = qtr + 4 * c;
-            const TC num = qtr == 0 ? p[4 * c] : (qtr == 1 ? p[4 * c + 1] : (qtr == 2 ? p[4 * c + 2] : p[4 * c + 3]));
-            const TC wold = qtr == 0 ? wr[4 * c] : (qtr == 1 ? wr[4 * c + 1] : (qtr == 2 ? wr[4 * c + 2] : wr[4 * c + 3]));
-            TC wn = 0;
-            if (s < ns && j < k) {
-              TC den = 0;
-#pragma unroll
-              for (int m = 0; m < KP; ++m) den = fma(wr[m], sHHt[j * KP + m], den);  // HHt symmetric
-              if (l1 > TC(0)) den += l1;                    // SK:616-617
-              if (l2 > TC(0)) den = den + l2 * wold;        // SK:618-619
-              if (den == TC(0)) den = TC(EPS32);            // SK:620
-              const TC qv = num / den;                      // SK:622
-              wn = wold * qv;                               // SK:629
-              W[(size_t)(tile * TS + s) * k + j] = wn;
-            }
-            sWn[s * KP + j] = wn;
-          }
-          if (SPLIT)
-            __builtin_amdgcn_wave_barrier();  // sWn rows of this wave feed its own A phase
-          else
-            __syncthreads();                  // wide rows: the A phase reads every wave's rows
-        }
-      }
+    phase12<TX, TC, KP, FT>(sX, sW, sWn, sHt, sHHt, W, tile, F, q, k, ns, s_beg, lane, do_loss, do_upd,
+                            l1, l2, loss64);
+    if (do_upd) {
+      if (SPLIT)
+        __builtin_amdgcn_wave_barrier();  // sWn rows of this wave feed its own A phase
+      else
+        __syncthreads();                  // wide rows: the A phase reads every wave's rows
     }
 
     if (do_acc) {
@@ -540,25 +561,24 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int NB_MAX = 8;  // 16-column blocks of [X | W'] (V <= 128)
 
 template <typename TX, int KP, int FT>
-__global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 3 : 4) : 2) void mu_pass_mfma_kernel(const TX* __restrict__ X,
+__global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 2 : (KP == 8 ? 3 : 4)) : 2) void mu_pass_mfma_kernel(const TX* __restrict__ X,
                                                             float* __restrict__ W,
-                                                            const float* __restrict__ Ht,
-                                                            const float* __restrict__ HHt,
+                                                            const double* __restrict__ Ht,
+                                                            const double* __restrict__ HHt,
                                                             double* __restrict__ partials,
-                                                            int64_t n_rows, int F_rt, int k, float l1,
-                                                            float l2, int flags, int64_t n_tiles) {
+                                                            int64_t n_rows, int F_rt, int k, double l1,
+                                                            double l2, int flags, int64_t n_tiles) {
   using TC = float;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int F = FT > 0 ? FT : F_rt;
-  const int nk1 = (F + 3) >> 2;        // phase-1 K-steps
   const int V = F + k;
   const int nb_cnt = (V + 15) >> 4;    // phase-3 column blocks
   const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC));
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
-  TC* sHHt = reinterpret_cast<TC*>(smem + L.hht);
+  double* sHt = reinterpret_cast<double*>(smem + L.ht);
+  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
   const int t = threadIdx.x;
@@ -570,25 +590,12 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 3 : 4) : 2) void mu_pass_m
   const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
 
-  for (int e = t; e < NWAVE * feat_per_wave(F) * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : TC(0);
+  for (int e = t; e < NWAVE * feat_per_wave(F) * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : 0.0;
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
   if (t < 4) {
     sX[TS * F + t] = TX{};
     reinterpret_cast<uint32_t*>(smem + L.zero)[t] = 0u;
   }
-  // phase-1 A operand Ht[4s+lk][ln]: held in VGPRs when the prefetch buffer leaves room for it
-  // (bf16 X), else read from the LDS copy of Ht each K-step
-  constexpr int NK1C = FT > 0 ? (FT + 3) / 4 : 1;
-  constexpr bool A1_REG = FT > 0 && sizeof(TX) == 2 && KP == 4;
-  float a1[A1_REG ? NK1C : 1];
-  if constexpr (A1_REG) {
-#pragma unroll
-    for (int st = 0; st < NK1C; ++st) {
-      const int f = 4 * st + lk;
-      a1[st] = (f < F && ln < KP) ? Ht[f * KP + ln] : 0.0f;
-    }
-  }
-
   // column blocks held in registers: exact for a compile-time F (k <= KP), NB_MAX otherwise
   constexpr int NBC = FT > 0 ? (FT + KP + 15) / 16 : NB_MAX;
   f32x4 acc[NBC];
@@ -610,69 +617,11 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 3 : 4) : 2) void mu_pass_m
       if (nt < n_tiles) prefetch_tile<PFT>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
     }
 
-    // ---- phase 1: d1[r] = num[s = s_beg + ln][j = 4*lk + r]
-    const int s = s_beg + ln;
-    f32x4 d1 = f32x4{0.f, 0.f, 0.f, 0.f};
-    {
-      const TX* xb = sX + (size_t)s * F + lk;
-      if constexpr (A1_REG) {
-#pragma unroll 7
-        for (int st = 0; st < NK1C; ++st)
-          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[st], to_c(xb[4 * st]), d1, 0, 0, 0);
-      } else if constexpr (FT > 0) {
-        const float* hb = sHt + lk * KP + ln;  // Ht[4st+lk][ln]; rows >= F and columns >= k are 0
-#pragma unroll 7
-        for (int st = 0; st < NK1C; ++st) {
-          const float a = ln < KP ? hb[4 * st * KP] : 0.0f;
-          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, to_c(xb[4 * st]), d1, 0, 0, 0);
-        }
-      } else {
-        for (int st = 0; st < nk1; ++st) {
-          const int f = 4 * st + lk;
-          const float a = (f < F && ln < KP) ? sHt[f * KP + ln] : 0.0f;
-          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, to_c(xb[4 * st]), d1, 0, 0, 0);
-        }
-      }
-    }
-
-    if (do_upd) {
-      // ---- phase 2: lanes with 4*lk < KP update components j = 4*lk + r of sample s
-      if (4 * lk < KP) {
-        float wr[KP];
-#pragma unroll
-        for (int m = 0; m < KP; ++m)
-          wr[m] = (k == KP) ? sW[s * KP + m] : ((m < k) ? sW[s * k + m] : 0.0f);
-        float wn[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = 4 * lk + r;
-          float wold = 0.0f;
-#pragma unroll
-          for (int m = 0; m < KP; ++m)
-            if (m == j) wold = wr[m];
-          float den = 0.0f;
-#pragma unroll
-          for (int m = 0; m < KP; ++m) den = fmaf(wr[m], sHHt[j * KP + m], den);  // HHt symmetric
-          if (l1 > 0.0f) den += l1;                    // SK:616-617
-          if (l2 > 0.0f) den = den + l2 * wold;        // SK:618-619
-          if (den == 0.0f) den = (float)EPS32;         // SK:620
-          const float qv = d1[r] / den;                // SK:622
-          wn[r] = (s < ns && j < k) ? wold * qv : 0.0f;  // SK:629
-          sWn[s * KP + j] = wn[r];
-        }
-        if (s < ns) {
-          float* wrow = W + (size_t)(tile * TS + s) * k + 4 * lk;
-          if (k == KP) {
-            *reinterpret_cast<f32x4*>(wrow) = f32x4{wn[0], wn[1], wn[2], wn[3]};
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              if (4 * lk + r < k) wrow[r] = wn[r];
-          }
-        }
-      }
-      __builtin_amdgcn_wave_barrier();  // this wave's sWn rows feed its own phase 3
-    }
+    // ---- phases 1+2 (wave-local, fp64; shared with mu_pass_kernel)
+    double loss_unused = 0.0;
+    phase12<TX, TC, KP, FT>(sX, sW, sWn, sHt, sHHt, W, tile, F, feat_per_wave(F), k, ns, s_beg, lane,
+                            false, do_upd, l1, l2, loss_unused);
+    if (do_upd) __builtin_amdgcn_wave_barrier();  // this wave's sWn rows feed its own phase 3
 
     if (do_acc) {
       // ---- phase 3: acc[nb][r] = Σ_s w'[s][4lk+r]·val[s][16nb+ln]
@@ -740,9 +689,8 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
-template <typename TC>
-__device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HHt, int F, int k,
-                                   int KP, double l1, double l2, int do_update, double* stats,
+__device__ void basis_update_block(const double* AB, double* H64, double* Ht, double* HHt, int F,
+                                   int k, int KP, double l1, double l2, int do_update, double* stats,
                                    double* lds) {
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -780,7 +728,7 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
   for (int e = t; e < F * KP; e += RED_NT) {
     const int f = e / KP;
     const int j = e - f * KP;
-    Ht[e] = j < k ? (TC)sH[j * F + f] : TC(0);
+    Ht[e] = j < k ? sH[j * F + f] : 0.0;
   }
   // HHt[j][m] = Σ_f H[j][f]·H[m][f]: one wave per entry, lanes over f, fixed-order shuffle tree
   for (int e = wave; e < KP * KP; e += NWV) {
@@ -793,7 +741,7 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
     }
     if (lane == 0) {
       sHH[e] = v;
-      HHt[e] = (TC)v;
+      HHt[e] = v;
     }
   }
   if (stats && have_ab) {
@@ -820,16 +768,15 @@ __device__ void basis_update_block(const double* AB, double* H64, TC* Ht, TC* HH
   }
 }
 
-template <typename TC>
 __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __restrict__ AB,
                                                               double* __restrict__ H64,
-                                                              TC* __restrict__ Ht,
-                                                              TC* __restrict__ HHt, int F, int k,
+                                                              double* __restrict__ Ht,
+                                                              double* __restrict__ HHt, int F, int k,
                                                               int KP, double l1, double l2,
                                                               int do_update, double* stats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  basis_update_block<TC>(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats,
-                         reinterpret_cast<double*>(smem));
+  basis_update_block(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats,
+                     reinterpret_cast<double*>(smem));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -842,12 +789,11 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
 // ------------------------------------------------------------------------------------------------
 struct UpdateArgs {
   double* H64;
-  void* Ht;
-  void* HHt;
+  double* Ht;
+  double* HHt;
   int F, k, KP;
   double l1, l2;
   double* stats;
-  int tc_double;
 };
 
 constexpr int RED_ROWS_PER_THREAD = 8;
@@ -915,12 +861,8 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
   if (!fuse) return;
   __syncthreads();
   double* scratch = upd + ((n_out + 1) & ~1);
-  if (ua.tc_double)
-    basis_update_block<double>(ab, ua.H64, (double*)ua.Ht, (double*)ua.HHt, ua.F, ua.k, ua.KP, ua.l1,
-                               ua.l2, 1, ua.stats, scratch);
-  else
-    basis_update_block<float>(ab, ua.H64, (float*)ua.Ht, (float*)ua.HHt, ua.F, ua.k, ua.KP, ua.l1,
-                              ua.l2, 1, ua.stats, scratch);
+  basis_update_block(ab, ua.H64, ua.Ht, ua.HHt, ua.F, ua.k, ua.KP, ua.l1, ua.l2, 1, ua.stats,
+                     scratch);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -994,15 +936,15 @@ static bool pick_tx(int KP, int F, int np, PassKernel* out) {
 }
 
 template <typename TX, int KP>
-static PassKernel make_mfma(int F) {
-  PassFn fn = F == 81 ? reinterpret_cast<PassFn>(&mu_pass_mfma_kernel<TX, KP, 81>)
-                      : reinterpret_cast<PassFn>(&mu_pass_mfma_kernel<TX, KP, 0>);
-  return PassKernel{fn, KP, 0, true, sizeof(TX), sizeof(float)};
+static PassKernel make_mfma(int) {
+  return PassKernel{reinterpret_cast<PassFn>(&mu_pass_mfma_kernel<TX, KP, 81>), KP, 0, true,
+                    sizeof(TX), sizeof(float)};
 }
 
-// The matrix-core pass serves fp32 / bf16 X whose [X | W] rows fit 8 column blocks (V <= 128).
+// The matrix-core pass serves fp32 / bf16 X on the compile-time IOP grid (F = 81, V <= 97);
+// other widths take mu_pass_kernel (its runtime-F MFMA form spilled registers).
 static bool pick_mfma(int x_dtype, int F, int k, PassKernel* out) {
-  if (F + k > 16 * NB_MAX || (x_dtype != CNMF_F32 && x_dtype != CNMF_BF16)) return false;
+  if (F != 81 || F + k > 16 * NB_MAX || (x_dtype != CNMF_F32 && x_dtype != CNMF_BF16)) return false;
   const int KP = k <= 4 ? 4 : (k <= 8 ? 8 : 16);
   const bool bf = x_dtype == CNMF_BF16;
   switch (KP) {
@@ -1095,7 +1037,7 @@ using namespace cnmf;
 
 extern "C" {
 
-int cnmf_abi_version(void) { return 100; }
+int cnmf_abi_version(void) { return 200; }
 
 const char* cnmf_last_error(void) { return g_err; }
 
@@ -1114,7 +1056,7 @@ int64_t cnmf_pass_blocks(int64_t n_rows, int n_features, int k, int x_dtype) {
   return nb;
 }
 
-int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, const void* HHt,
+int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, const double* HHt,
                         double* partials, int64_t n_rows, int n_features, int k, double l1_W,
                         double l2_W, int flags, void* stream) {
   if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
@@ -1146,15 +1088,8 @@ int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, con
   const int64_t n_tiles = (n_rows + TS - 1) / TS;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   int F = n_features;
-  if (pk.sc == sizeof(double)) {
-    double l1 = l1_W, l2 = l2_W;
-    void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1, &l2, &flags, (void*)&n_tiles};
-    HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
-  } else {
-    float l1 = (float)l1_W, l2 = (float)l2_W;
-    void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1, &l2, &flags, (void*)&n_tiles};
-    HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
-  }
+  void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&n_tiles};
+  HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
   return CNMF_OK;
 }
 
@@ -1187,48 +1122,37 @@ int cnmf_reduce_partials(const double* partials, int64_t n_parts, int n_out, dou
                        reinterpret_cast<hipStream_t>(stream));
 }
 
-static int check_update_args(const double* H64, const void* Ht, const void* HHt, int w_dtype, int F,
-                             int k) {
+static int check_update_args(const double* H64, const double* Ht, const double* HHt, int F, int k) {
   if (!H64 || !Ht || !HHt) return set_err(CNMF_ERR_ARG, "null pointer argument");
   if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
   if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
-  if (w_dtype != CNMF_F32 && w_dtype != CNMF_F64) return set_err(CNMF_ERR_ARG, "w_dtype must be F32/F64");
   return CNMF_OK;
 }
 
-int cnmf_basis_update(const double* AB, double* H64, void* Ht, void* HHt, int w_dtype,
-                      int n_features, int k, double l1_H, double l2_H, int do_update,
-                      double* stats, void* stream) {
-  int st = check_update_args(H64, Ht, HHt, w_dtype, n_features, k);
+int cnmf_basis_update(const double* AB, double* H64, double* Ht, double* HHt, int n_features, int k,
+                      double l1_H, double l2_H, int do_update, double* stats, void* stream) {
+  int st = check_update_args(H64, Ht, HHt, n_features, k);
   if (st) return st;
   if (do_update && !AB) return set_err(CNMF_ERR_ARG, "AB required for do_update");
   const int KP = padded_k(k);
   const size_t lds = update_lds_doubles(n_features, k, KP) * sizeof(double);
   if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the update kernel");
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (w_dtype == CNMF_F64) {
-    if (lds > 64 * 1024)
-      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&basis_update_kernel<double>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(basis_update_kernel<double>, dim3(1), dim3(RED_NT), lds, s, AB, H64,
-                       (double*)Ht, (double*)HHt, n_features, k, KP, l1_H, l2_H, do_update, stats);
-  } else {
-    if (lds > 64 * 1024)
-      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&basis_update_kernel<float>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(basis_update_kernel<float>, dim3(1), dim3(RED_NT), lds, s, AB, H64,
-                       (float*)Ht, (float*)HHt, n_features, k, KP, l1_H, l2_H, do_update, stats);
-  }
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&basis_update_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(basis_update_kernel, dim3(1), dim3(RED_NT), lds,
+                     reinterpret_cast<hipStream_t>(stream), AB, H64, Ht, HHt, n_features, k, KP, l1_H,
+                     l2_H, do_update, stats);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }
 
 int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, uint32_t* counter,
-                       double* AB, double* H64, void* Ht, void* HHt, int w_dtype, int n_features,
-                       int k, double l1_H, double l2_H, double* stats, void* stream) {
-  int st = check_update_args(H64, Ht, HHt, w_dtype, n_features, k);
+                       double* AB, double* H64, double* Ht, double* HHt, int n_features, int k,
+                       double l1_H, double l2_H, double* stats, void* stream) {
+  int st = check_update_args(H64, Ht, HHt, n_features, k);
   if (st) return st;
-  UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats, w_dtype == CNMF_F64};
+  UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats};
   return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,
                        reinterpret_cast<hipStream_t>(stream));
 }
@@ -1244,12 +1168,11 @@ int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, vo
   return CNMF_OK;
 }
 
-int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, void* Ht,
-                       void* HHt, double* partials, int64_t n_parts, double* stage,
+int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
+                       double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
                        void* const* pass_events, void* stream) {
-  const int w_dtype = x_dtype == CNMF_F64 ? CNMF_F64 : CNMF_F32;
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   for (int it = 0; it < n_iter; ++it) {
     if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it]), hs));
@@ -1257,8 +1180,8 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                                  l2_W, CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE, stream);
     if (st) return st;
     if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it + 1]), hs));
-    st = cnmf_reduce_update(partials, n_parts, stage, counter, AB, H64, Ht, HHt, w_dtype,
-                            n_features, k, l1_H, l2_H, stats, stream);
+    st = cnmf_reduce_update(partials, n_parts, stage, counter, AB, H64, Ht, HHt, n_features, k, l1_H,
+                            l2_H, stats, stream);
     if (st) return st;
   }
   return CNMF_OK;

@@ -59,7 +59,6 @@ class MUPlan:
         self.k = int(n_components)
         self.xdt = _XDT[X.dtype]
         self.tc = torch.float64 if X.dtype == torch.float64 else torch.float32
-        self.wdt = _lib.F64 if self.tc == torch.float64 else _lib.F32
         self.l1_W, self.l2_W, self.l1_H, self.l2_H = map(float, (l1_W, l2_W, l1_H, l2_H))
         self.group = group
         self.world = 1
@@ -78,8 +77,8 @@ class MUPlan:
         dev, f64 = self.device, torch.float64
         self.W = torch.empty((self.n_rows, self.k), dtype=self.tc, device=dev)
         self.H64 = torch.zeros((self.k, self.F), dtype=f64, device=dev)
-        self.Ht = torch.zeros((self.F, KP), dtype=self.tc, device=dev)
-        self.HHt = torch.zeros((KP, KP), dtype=self.tc, device=dev)
+        self.Ht = torch.zeros((self.F, KP), dtype=f64, device=dev)
+        self.HHt = torch.zeros((KP, KP), dtype=f64, device=dev)
         self.partials = torch.zeros((max(self.n_parts, 1), self.n_out), dtype=f64, device=dev)
         self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out)), dtype=f64, device=dev)
         self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
@@ -102,8 +101,8 @@ class MUPlan:
     def refresh_basis(self):
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_basis_update(None, _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
-                                             self.wdt, self.F, self.k, 0.0, 0.0, 0, None,
-                                             self._stream()), "cnmf_basis_update")
+                                             self.F, self.k, 0.0, 0.0, 0, None, self._stream()),
+                  "cnmf_basis_update")
 
     # -- launches ------------------------------------------------------------------------------
     def sample_pass(self, flags: int):
@@ -122,9 +121,8 @@ class MUPlan:
     def basis_update(self):
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_basis_update(_ptr(self.AB), _ptr(self.H64), _ptr(self.Ht),
-                                             _ptr(self.HHt), self.wdt, self.F, self.k, self.l1_H,
-                                             self.l2_H, 1, _ptr(self.stats), self._stream()),
-                  "cnmf_basis_update")
+                                             _ptr(self.HHt), self.F, self.k, self.l1_H, self.l2_H, 1,
+                                             None, self._stream()), "cnmf_basis_update")
 
     def _allreduce(self, t: torch.Tensor):
         if self.world > 1:

@@ -8,10 +8,12 @@
  * Each entry point names the SK lines it takes over; INTEGRATION.md shows the ctypes binding.
  *
  * Layout (sklearn naming, samples-major): X[N][F] row-major, W[N][k], H[k][F].
- * The pass computes in the "compute type" TC of its X dtype: fp32 for CNMF_F32 and CNMF_BF16,
- * fp64 for CNMF_F64.  Basis-side state is fp64 (H64) with TC copies for the pass:
+ * W has the "compute type" TC of the X dtype: fp32 for CNMF_F32 and CNMF_BF16, fp64 for CNMF_F64;
+ * the per-sample update itself is evaluated in fp64 for every dtype.  All
+ * basis-side state is fp64:
+ *   H64[k][F]   = the basis (master copy)
  *   Ht [F][KP]  = H transposed, zero-padded to KP = cnmf_padded_k(k) columns
- *   HHt[KP][KP] = H·Hᵀ (from fp64 H), zero-padded.
+ *   HHt[KP][KP] = H·Hᵀ, zero-padded.
  *   AB [k][F+k] = the reduced accumulators: AB[j][f] = (WᵀX)[j][f], AB[j][F+m] = (WᵀW)[j][m].
  *
  * Conventions.  All pointers are caller-owned device pointers (no allocation in any call except
@@ -67,8 +69,8 @@ int64_t cnmf_stage_doubles(int n_out);
  *   and, with CNMF_PASS_ACCUMULATE, per-workgroup fp64 partials of [WᵀX | WᵀW] using the NEW W,
  *   written to partials[block][k*(F+k)].  With CNMF_PASS_LOSS alone it writes per-workgroup
  *   partials of ‖X − W·H‖² (partials[block][0]) and changes nothing.
- *   X: [n_rows][F] of x_dtype; W: [n_rows][k] of TC; Ht, HHt: TC as above. */
-int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const void* Ht, const void* HHt,
+ *   X: [n_rows][F] of x_dtype; W: [n_rows][k] of TC; Ht, HHt: fp64 as above. */
+int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, const double* HHt,
                         double* partials, int64_t n_rows, int n_features, int k, double l1_W,
                         double l2_W, int flags, void* stream);
 
@@ -80,25 +82,24 @@ int cnmf_reduce_partials(const double* partials, int64_t n_parts, int n_out, dou
 
 /* The basis update on the reduced AB (replaces SK:639-726 after the reductions):
  *   den = (WᵀW)·H (+l1_H) (+l2_H·H), den==0 -> float32 eps, H <- H·(WᵀX/den)   (do_update=1)
- * then refreshes Ht and HHt (TC = w_dtype: CNMF_F32 or CNMF_F64) from the fp64 H64.  With
- * do_update=0 it only derives Ht/HHt from H64 (first iteration, transform).  stats (may be NULL)
- * receives {<AB_A, H>, <AB_B, H·Hᵀ>} for the cheap loss ‖X‖² − 2<A,H> + <B,HHᵀ>. */
-int cnmf_basis_update(const double* AB, double* H64, void* Ht, void* HHt, int w_dtype,
-                      int n_features, int k, double l1_H, double l2_H, int do_update,
-                      double* stats, void* stream);
+ * then refreshes Ht and HHt from the fp64 H64.  With do_update=0 it only derives Ht/HHt from H64
+ * (first iteration, transform; AB may then be NULL).  stats (may be NULL) receives
+ * {<AB_A, H>, <AB_B, H·Hᵀ>} for the cheap loss ‖X‖² − 2<A,H> + <B,HHᵀ>. */
+int cnmf_basis_update(const double* AB, double* H64, double* Ht, double* HHt, int n_features, int k,
+                      double l1_H, double l2_H, int do_update, double* stats, void* stream);
 
 /* cnmf_reduce_partials followed, in the same launch (last-arriving workgroup), by
  * cnmf_basis_update(do_update=1): the single-GPU iteration tail. */
 int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, uint32_t* counter,
-                       double* AB, double* H64, void* Ht, void* HHt, int w_dtype, int n_features,
-                       int k, double l1_H, double l2_H, double* stats, void* stream);
+                       double* AB, double* H64, double* Ht, double* HHt, int n_features, int k,
+                       double l1_H, double l2_H, double* stats, void* stream);
 
 /* n_iter single-GPU MU iterations (pass + reduce_update each) launched back to back with no host
  * synchronisation: the body of SK:831-870 for tol == 0 stretches.  pass_events (may be NULL):
  * 2*n_iter caller-created hipEvent_t recorded on `stream` right before / after each sample pass
  * (live per-launch timing of the dominant kernel for the roofline report). */
-int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, void* Ht,
-                       void* HHt, double* partials, int64_t n_parts, double* stage,
+int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
+                       double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
                        void* const* pass_events, void* stream);

@@ -70,7 +70,7 @@ def main():
     def tail():
         _lib.check(lib.cnmf_reduce_update(plan.partials.data_ptr(), plan.n_parts, plan.stage.data_ptr(),
                                           plan.counter.data_ptr(), plan.AB.data_ptr(), plan.H64.data_ptr(),
-                                          plan.Ht.data_ptr(), plan.HHt.data_ptr(), plan.wdt, plan.F, plan.k,
+                                          plan.Ht.data_ptr(), plan.HHt.data_ptr(), plan.F, plan.k,
                                           0.0, 0.0, plan.stats.data_ptr(), s))
     out["reduce_update_us"] = round(timed(tail, a.reps, stream), 2)
     us = timed(lambda: plan.iterate(1), a.reps, stream)

@@ -105,7 +105,7 @@ struct PassLds {
   size_t region0;  // X tile [TS][F] (+4 zero elements), later the cross-wave reduction scratch
   size_t w;        // old-W tile, flat [ns][k]
   size_t wn;       // new-W tile, [TS][KP] (zero for j >= k and for invalid samples)
-  size_t ht;       // Ht (fp64), [4*q][KP], rows >= F zero (q = ceil(F/4): a lane sums q features)
+  size_t ht;       // Ht (compute type), [4*q][KP], rows >= F zero (q = ceil(F/4) per lane)
   size_t hht;      // HHt (fp64), [KP][KP]
   size_t zero;     // 16 zero bytes (source of the idle lanes of the A phase)
   size_t total;
@@ -121,7 +121,7 @@ __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc)
   L.w = L.region0;
   L.wn = L.w + align16((size_t)TS * KP * sc);
   L.ht = L.wn + align16((size_t)TS * KP * sc);
-  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sizeof(double));
+  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sc);
   L.zero = L.hht + align16((size_t)KP * KP * sizeof(double));
   L.total = L.zero + 16;
   return L;
@@ -217,13 +217,13 @@ __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
 // Phases 1+2 of a tile, shared by both pass kernels; wave-local (wave w owns samples
 // [16w, 16w+16), lane = (sample s = lane/4, feature quarter qtr = lane%4)) and in fp64.
 //
-// Why fp64: the 81-term dot products num = x·Hᵀ summed in fp32 leave a rounding error that is
+// Precision: a long fp32 chain for the dot products num = x·Hᵀ leaves a rounding error that is
 // nearly the SAME every iteration once H settles, so it drifts coherently instead of averaging out:
-// 500 iterations of k=8 MU end 1.8e-5 (rel. Frobenius) from the fp64 oracle with fp32 sums and
-// 6e-7 with fp64 sums (NumPy emulation of this kernel's arithmetic).  An fp32
-// product is exact in fp64, so each step is one v_fma_f64 on the converted x.
-//   phase 1: lane sums its quarter of x[s]·Ht (Ht rows >= F are zero), quad shuffles in the fixed
-//            order (q0+q1)+(q2+q3) complete num[s][0..KP) in every lane of the quad;
+// 500 iterations of k=8 MU end 1.8e-5 (rel. Frobenius) from the fp64 oracle with 81-term fp32
+// chains, 5.5e-7 with 7-term fp32 chains folded into fp64 (NumPy emulation of this kernel's
+// arithmetic) — as good as all-fp64, at fp32 VALU cost.
+//   phase 1: lane sums its quarter of x[s]·Ht (Ht rows >= F are zero) in fp32 chains of 7 folded
+//            into fp64; quad shuffles in the fixed order (q0+q1)+(q2+q3) complete num[s][0..KP);
 //   phase 2: lane (s, qtr) updates components j = qtr + 4c:
 //            den = Σ_m w[s][m]·HHt[j][m] (+l1)(+l2·w), den==0 -> eps32, w' = w·(num/den) in fp64,
 //            rounded once to TC, stored to HBM and to the LDS row sWn[s] (A phase input).
@@ -231,7 +231,7 @@ __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
 // ------------------------------------------------------------------------------------------------
 template <typename TX, typename TC, int KP, int FT>
 __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __restrict__ sW,
-                                        TC* __restrict__ sWn, const double* __restrict__ sHt,
+                                        TC* __restrict__ sWn, const TC* __restrict__ sHt,
                                         const double* __restrict__ sHHt, TC* __restrict__ W,
                                         int64_t tile, int F, int q, int k, int ns, int s_beg,
                                         int lane, bool do_loss, bool do_upd, double l1, double l2,
@@ -240,7 +240,7 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
   const int s = s_beg + (lane >> 2);
   const int fb = qtr * q;
   const TX* xr = sX + (size_t)s * F + fb;
-  const double* hb = sHt + (size_t)fb * KP;
+  const TC* hb = sHt + (size_t)fb * KP;
   if (do_loss) {
     double w[KP];
 #pragma unroll
@@ -250,7 +250,7 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
     for (int f = 0; f < nf; ++f) {
       double wh = 0.0;
 #pragma unroll
-      for (int j = 0; j < KP; ++j) wh = fma(w[j], hb[f * KP + j], wh);
+      for (int j = 0; j < KP; ++j) wh = fma(w[j], (double)hb[f * KP + j], wh);
       const double r = (double)to_c(xr[f]) - wh;
       part = fma(r, r, part);
     }
@@ -259,23 +259,42 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
     if (qtr == 0 && s < ns) loss64 += part;
     return;
   }
+  // fp32 (TC) FMA chains of PCH features folded into fp64 (see the precision note above)
+  constexpr int PCH = 7;
   double p[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) p[j] = 0.0;
   if constexpr (FT > 0) {
     constexpr int QF = (FT + NWAVE - 1) / NWAVE;
-#pragma unroll 2
-    for (int f = 0; f < QF; ++f) {
-      const double xv = (double)to_c(xr[f]);
+#pragma unroll 1
+    for (int f0 = 0; f0 < QF; f0 += PCH) {
+      TC pc[KP];
 #pragma unroll
-      for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+      for (int j = 0; j < KP; ++j) pc[j] = TC(0);
+#pragma unroll
+      for (int ff = 0; ff < PCH; ++ff) {
+        if (f0 + ff < QF) {
+          const TC xv = to_c(xr[f0 + ff]);
+#pragma unroll
+          for (int j = 0; j < KP; ++j) pc[j] = fma(xv, hb[(f0 + ff) * KP + j], pc[j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < KP; ++j) p[j] += (double)pc[j];
     }
   } else {
-#pragma unroll 4
-    for (int f = 0; f < q; ++f) {
-      const double xv = (double)to_c(xr[f]);
+    for (int f0 = 0; f0 < q; f0 += PCH) {
+      TC pc[KP];
 #pragma unroll
-      for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+      for (int j = 0; j < KP; ++j) pc[j] = TC(0);
+      const int fe = min(q, f0 + PCH);
+      for (int f = f0; f < fe; ++f) {
+        const TC xv = to_c(xr[f]);
+#pragma unroll
+        for (int j = 0; j < KP; ++j) pc[j] = fma(xv, hb[f * KP + j], pc[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < KP; ++j) p[j] += (double)pc[j];
     }
   }
 #pragma unroll
@@ -351,7 +370,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  double* sHt = reinterpret_cast<double*>(smem + L.ht);
+  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
@@ -365,7 +384,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
 
   // basis-side constants into LDS once per launch (Ht zero-padded to 4q rows)
-  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : 0.0;
+  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? (TC)Ht[e] : TC(0);
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
   if (t < 4) {
     sX[TS * F + t] = TX{};
@@ -577,7 +596,7 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 2 : (KP == 8 ? 3 : 4)) : 2
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  double* sHt = reinterpret_cast<double*>(smem + L.ht);
+  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
@@ -590,7 +609,7 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 2 : (KP == 8 ? 3 : 4)) : 2
   const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
 
-  for (int e = t; e < NWAVE * feat_per_wave(F) * KP; e += NT) sHt[e] = e < F * KP ? Ht[e] : 0.0;
+  for (int e = t; e < NWAVE * feat_per_wave(F) * KP; e += NT) sHt[e] = e < F * KP ? (TC)Ht[e] : TC(0);
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
   if (t < 4) {
     sX[TS * F + t] = TX{};

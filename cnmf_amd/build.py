@@ -31,17 +31,23 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > out_m for d in deps if os.path.exists(d))
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
-    if not force and not needs_build():
+def build(verbose: bool = False, force: bool = False, stamps: bool = False) -> str:
+    """Compile libcnmf_hip.so (or, with stamps=True, the diagnostic libcnmf_hip_stamps.so whose pass
+    kernel records per-phase s_memtime sums; never used by the product)."""
+    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
+    if not force and not stamps and not needs_build():
         return OUT
     cmd = [hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp", SRC]
+           "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
+    if stamps:
+        cmd.insert(1, "-DCNMF_STAMPS")
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv))
+    print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv,
+                stamps="--stamps" in sys.argv))

@@ -214,6 +214,35 @@ __device__ __forceinline__ T lds_at(const unsigned char* smem, uint32_t off) {
 
 
 // ------------------------------------------------------------------------------------------------
+// Diagnostic phase stamps (built only with -DCNMF_STAMPS into a separate .so; never in the real
+// kernel): per wave, s_memtime deltas between the phase boundaries of every tile are summed in
+// registers and added once per wave into g_stamps[slot] (MI355X guide §7 "In-kernel stamps").
+// ------------------------------------------------------------------------------------------------
+#ifdef CNMF_STAMPS
+__device__ unsigned long long g_stamps[16];
+#define STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long st_t0 = 0;
+#define STAMP(slot)                                                                   \
+  do {                                                                                \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    unsigned long long st_t;                                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t) :: "memory");    \
+    __builtin_amdgcn_sched_barrier(0);                                                \
+    if (slot > 0) st_acc[slot] += st_t - st_t0;                                       \
+    st_t0 = st_t;                                                                     \
+  } while (0)
+#define STAMP_FLUSH                                                                   \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0)                                                      \
+      for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamps[i_], st_acc[i_]);           \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[8], 1ull);                       \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(slot) do {} while (0)
+#define STAMP_FLUSH do {} while (0)
+#endif
+
+// ------------------------------------------------------------------------------------------------
 // Phases 1+2 of a tile, shared by both pass kernels; wave-local (wave w owns samples
 // [16w, 16w+16), lane = (sample s = lane/4, feature quarter qtr = lane%4)) and in fp64.
 //
@@ -397,6 +426,7 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
 #pragma unroll
     for (int j = 0; j < KP; ++j) acc[i][j] = TC(0);
   double loss64 = 0.0;
+  STAMP_DECL
 
   // 16-byte chunks per thread per tile: exact for a compile-time F, PF otherwise
   constexpr int PFT = FT > 0 ? (int)((TS * FT * sizeof(TX) + TS * KP * sizeof(TC) + 16 * NT - 1) / (16 * NT)) : PF;
@@ -410,8 +440,11 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   for (; tile < n_tiles; tile += gridDim.x) {
     const TileGeom g = tile_geom(X, W, tile, n_rows, F, k);
     const int ns = g.ns;
+    STAMP(0);
     stage_tile<TX, TC, PFT>(smem, L.w, g, pf, t, F);
+    STAMP(1);  // 1: wait for this tile's loads + LDS writes
     __syncthreads();
+    STAMP(2);  // 2: staging barrier
 
     // ---- issue the next tile's loads; they stay in flight through this tile's compute
     {
@@ -420,11 +453,13 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
         prefetch_tile<PFT>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
       }
     }
+    STAMP(3);  // 3: prefetch issue
 
     // ---- phases 1+2 (wave-local, fp64)
     const int s_beg = wave * (TS / NWAVE);
     phase12<TX, TC, KP, FT>(sX, sW, sWn, sHt, sHHt, W, tile, F, q, k, ns, s_beg, lane, do_loss, do_upd,
                             l1, l2, loss64);
+    STAMP(4);  // 4: phases 1+2
     if (do_upd) {
       if (SPLIT)
         __builtin_amdgcn_wave_barrier();  // sWn rows of this wave feed its own A phase
@@ -511,8 +546,11 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
         }
       }
     }
+    STAMP(5);  // 5: phase 3
     __syncthreads();  // LDS tiles are rewritten by the next iteration
+    STAMP(6);  // 6: end-of-tile barrier
   }
+  STAMP_FLUSH;
 
   // ---- per-workgroup partial rows (fp64 combine of the 4 waves' fp32 accumulators)
   if (do_acc) {
@@ -1175,6 +1213,17 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
   return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,
                        reinterpret_cast<hipStream_t>(stream));
 }
+
+#ifdef CNMF_STAMPS
+int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z, sizeof(z)));
+  }
+  return CNMF_OK;
+}
+#endif
 
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream) {
   if (!buf || !out || bytes < 16 || n_blocks < 1)

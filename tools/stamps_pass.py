@@ -1,0 +1,55 @@
+"""Per-phase cycle breakdown of the VALU pass kernel from the diagnostic stamps build.
+
+    python -m cnmf_amd.build --stamps
+    CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_stamps.so CNMF_FORCE_VALU=1 python tools/stamps_pass.py
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+NAMES = ["", "stage wait+LDS write", "staging barrier", "prefetch issue", "phases 1+2", "phase 3 (A)",
+         "end barrier"]
+
+
+def main():
+    import torch
+    from cnmf_amd import _lib
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    k = int(os.environ.get("K", "4"))
+    X = iop_spectra(1_000_000, 81, seed=0, dtype=np.float32)
+    W0, H0 = random_init(X, k, 42)
+    lib = _lib.load()
+    fn = lib.cnmf_debug_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    fn.restype = ctypes.c_int
+    plan = MUPlan(torch.from_numpy(X).cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.iterate(3)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 16)()
+    fn(buf, 1)
+    n = 20
+    for flags in (3, 1):
+        plan.iterate(n) if flags == 3 else [plan.sample_pass(1) for _ in range(n)]
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        waves = buf[8]
+        tiles_per_wave = (plan.n_rows / 64) / plan.n_parts
+        out = {"flags": flags, "waves": waves, "tiles_per_wave": round(tiles_per_wave, 2)}
+        tot = 0
+        for i in range(1, 7):
+            cyc = buf[i] / waves / tiles_per_wave
+            tot += cyc
+            out[NAMES[i]] = round(cyc, 1)
+        out["total_cycles_per_tile"] = round(tot, 1)
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -734,6 +734,244 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 2 : (KP == 8 ? 3 : 4)) : 2
 }
 
 // ------------------------------------------------------------------------------------------------
+// The sample-lane pass: the IOP grid's headline shape (F = 81, k = 4, fp32 X and W), full tiles.
+//
+// mu_pass_kernel spends most of its issue slots and LDS cycles on moving data between lane
+// layouts (Hᵀ re-read by every sample quarter, quad shuffles of the partial dot products, and an
+// A phase that re-reads the whole X tile from LDS with 85 of 128 lanes busy).  Here lane = sample
+// in every phase that touches X, so each X element is read from LDS exactly once and stays in a
+// register from the dot product to the accumulation:
+//
+//   phase 1  wave w owns features [21w, 21w+21) (wave 3: 63..80 plus three zero Hᵀ rows), lane s
+//            owns sample s of the 64-sample tile: xv[c] = x[s][21w+c] (conflict-free ds_read_b32,
+//            row stride 81 is odd), partial num_w[s][j] = Σ_c xv[c]·Ht[21w+c][j] as fp32 chains of
+//            7 folded into fp64 (the precision note above phase12), written to LDS (32 B per lane).
+//   phase 2  lane (s = 16w + lane/4, j = lane%4): num = (P0+P1)+(P2+P3) (the same fp64 sum order as
+//            phase12's quad shuffles), den = Σ_m w[s][m]·HHt[j][m] (+l1)(+l2·w), eps32, w' = w·num/den
+//            in fp64 (SK:526-631) -> W in HBM (64 consecutive floats per wave) and LDS.
+//   phase 3  lane = sample again: acc[c][j] += w'[s][j]·xv[c] on the registers of phase 1; wave 3
+//            swaps its three padding columns for the W' columns 81..83, and the last column of
+//            B = W'ᵀW' comes from its symmetry (B[j][3] = B[3][j]) plus one Σ w'3² register.
+//            (SK:639-640 for the updated W.)
+//
+// A tile therefore costs per wave 21 x reads + 21 broadcast Hᵀ reads + 6 small LDS accesses,
+// about 200 VALU and 2 barriers.  The 21×4 (+1) fp32 accumulators of a lane (fp32 chains of one sample
+// per tile over the workgroup's tiles) are tree-summed across the wave with DPP at the end of the
+// launch and written as ONE fp64 partial row [k][F+k] per workgroup, like mu_pass_kernel.
+// Registers: acc 85 + xv 21 + the next tile's 16-byte prefetch 24 -> three waves per SIMD.
+// ------------------------------------------------------------------------------------------------
+namespace sl {
+constexpr int F = 81, K = 4, V = F + K;
+constexpr int NF = 21;                     // features per wave in phase 1 (4 × 21 = 84 ≥ 81)
+constexpr int NC = 21;                     // accumulator columns per wave (wave 3: 18 X + W'0..2)
+constexpr int NR = NC * 4 + 1;             // row-sum values per wave (+ wave 3's Σ w'3²)
+constexpr int XB = TS * F * 4;             // 20736 bytes of X per tile
+constexpr int WB = TS * K * 4;             // 1024 bytes of W per tile
+constexpr int NXC = XB / 16;               // 1296 X chunks
+constexpr int NCH = (XB + WB) / 16;        // 1360 chunks per tile
+constexpr int PFN = (NCH + NT - 1) / NT;   // 6 chunks per thread
+constexpr int RED = NWAVE * 4 * NR * 4;    // end-of-launch row sums: [wave][row][NR] floats
+// LDS carve (bytes)
+constexpr int L_X = 0;                                      // X tile + 16 zero bytes; later RED
+constexpr int L_W = ((XB + 16 > RED ? XB + 16 : RED) + 15) / 16 * 16;  // W tiles, double-buffered
+constexpr int L_P = L_W + 2 * WB;                           // phase-1 partials [wave][s][j] fp64
+constexpr int L_WN = L_P + NWAVE * TS * K * 8;              // new W tile [s][j] fp32
+constexpr int L_HT = L_WN + TS * K * 4;                     // Hᵀ [84][4] fp32 (rows >= 81 zero)
+constexpr int L_HHT = L_HT + NWAVE * NF * K * 4;            // HHᵀ [4][4] fp64
+constexpr int L_TOTAL = L_HHT + K * K * 8;
+static_assert(PFN == 6 && NCH - (PFN - 1) * NT == 80, "prefetch layout assumes 1360 chunks");
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  const int m = __builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true);
+  return v + __int_as_float(m);
+}
+
+// 16-byte chunk i of this thread for tile `tile`: X chunk (t + 256 i), or for i = 5 and t < 80 the
+// tail of X (t < 16) / the W tile (16 <= t < 80); threads t >= 80 re-read X chunk t (not stored).
+__device__ __forceinline__ void sl_prefetch(u32x4 (&pf)[PFN], const unsigned char* __restrict__ X,
+                                            const unsigned char* __restrict__ W, int64_t tile, int t) {
+  const unsigned char* xs = X + (size_t)tile * XB + 16 * t;
+#pragma unroll
+  for (int i = 0; i < PFN - 1; ++i)
+    pf[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xs + 4096 * i));
+  const unsigned char* last = t < 16 ? xs + 4096 * (PFN - 1)
+                                     : (t < 80 ? W + (size_t)tile * WB + 16 * (t - 16) : xs);
+  pf[PFN - 1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(last));
+}
+
+__device__ __forceinline__ void sl_stage(unsigned char* smem, int wpar, const u32x4 (&pf)[PFN], int t) {
+#pragma unroll
+  for (int i = 0; i < PFN - 1; ++i)
+    *reinterpret_cast<u32x4*>(smem + L_X + 16 * t + 4096 * i) = pf[i];
+  if (t < 80) {
+    unsigned char* dst = t < 16 ? smem + L_X + 16 * t + 4096 * (PFN - 1)
+                                : smem + L_W + wpar * WB + 16 * (t - 16);
+    *reinterpret_cast<u32x4*>(dst) = pf[PFN - 1];
+  }
+}
+
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
+  __builtin_amdgcn_s_barrier();
+}
+}  // namespace sl
+
+__global__ __launch_bounds__(NT, 3) void mu_pass_sl_kernel(const float* __restrict__ X,
+                                                          float* __restrict__ W,
+                                                          const double* __restrict__ Ht,
+                                                          const double* __restrict__ HHt,
+                                                          double* __restrict__ partials,
+                                                          int64_t n_tiles, double l1, double l2) {
+  using namespace sl;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(X);
+  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(W);
+  float* sHt = reinterpret_cast<float*>(smem + L_HT);
+  double* sHHt = reinterpret_cast<double*>(smem + L_HHT);
+  double* sP = reinterpret_cast<double*>(smem + L_P);
+  float* sWn = reinterpret_cast<float*>(smem + L_WN);
+
+  for (int e = t; e < NWAVE * NF * K; e += NT) sHt[e] = e < F * K ? (float)Ht[e] : 0.f;
+  if (t < K * K) sHHt[t] = HHt[t];
+  if (t < 4) reinterpret_cast<float*>(smem + L_X + XB)[t] = 0.f;
+
+  float acc[NC][K];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[c][j] = 0.f;
+  float acc33 = 0.f;
+
+  const int64_t G = gridDim.x;
+  int64_t tile = blockIdx.x;
+  u32x4 pf[PFN];
+  // prologue: tile `tile` -> LDS, tile + G -> registers
+  sl_prefetch(pf, Xb, Wb, tile, t);
+  sl_stage(smem, 0, pf, t);
+  if (tile + G < n_tiles) sl_prefetch(pf, Xb, Wb, tile + G, t);
+  lds_barrier();
+
+  const float* sX = reinterpret_cast<const float*>(smem + L_X);
+  const int fbase = NF * wave;
+  int wpar = 0;
+  for (; tile < n_tiles; tile += G, wpar ^= 1) {
+    // ---- phase 1: lane = sample, wave = 21 features
+    float xv[NC];
+    {
+      const float* xr = sX + lane * F + fbase;
+#pragma unroll
+      for (int c = 0; c < NF; ++c) xv[c] = xr[c];
+      double p[K] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int c0 = 0; c0 < NF; c0 += 7) {
+        float pc[K] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = c0; c < c0 + 7; ++c) {
+          const float4 h = *reinterpret_cast<const float4*>(sHt + (fbase + c) * K);
+          pc[0] = fmaf(xv[c], h.x, pc[0]);
+          pc[1] = fmaf(xv[c], h.y, pc[1]);
+          pc[2] = fmaf(xv[c], h.z, pc[2]);
+          pc[3] = fmaf(xv[c], h.w, pc[3]);
+        }
+#pragma unroll
+        for (int j = 0; j < K; ++j) p[j] += (double)pc[j];
+      }
+      double* pw = sP + ((size_t)wave * TS + lane) * K;
+      *reinterpret_cast<double2*>(pw) = make_double2(p[0], p[1]);
+      *reinterpret_cast<double2*>(pw + 2) = make_double2(p[2], p[3]);
+    }
+    lds_barrier();  // A: every wave is done reading this X tile and has written its partials
+
+    // ---- phase 2: lane = (sample 16w + lane/4, component lane%4)
+    {
+      const int s = 16 * wave + (lane >> 2);
+      const int j = lane & 3;
+      const double num = (sP[(0 * TS + s) * K + j] + sP[(1 * TS + s) * K + j]) +
+                         (sP[(2 * TS + s) * K + j] + sP[(3 * TS + s) * K + j]);
+      const float* sWo = reinterpret_cast<const float*>(smem + L_W + wpar * WB);
+      const float4 wv = *reinterpret_cast<const float4*>(sWo + s * K);
+      const double wold = (double)sWo[s * K + j];
+      const double* hr = sHHt + j * K;
+      double den = 0.0;
+      den = fma((double)wv.x, hr[0], den);
+      den = fma((double)wv.y, hr[1], den);
+      den = fma((double)wv.z, hr[2], den);
+      den = fma((double)wv.w, hr[3], den);
+      if (l1 > 0.0) den += l1;              // SK:616-617
+      if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
+      if (den == 0.0) den = EPS32;          // SK:620
+      const float wn = (float)(wold * (num / den));  // SK:622-629
+      W[((size_t)tile * TS + s) * K + j] = wn;
+      sWn[s * K + j] = wn;
+    }
+    // ---- stage the next tile (X region is free since barrier A) and prefetch the one after
+    if (tile + G < n_tiles) {
+      sl_stage(smem, wpar ^ 1, pf, t);
+      if (tile + 2 * G < n_tiles) sl_prefetch(pf, Xb, Wb, tile + 2 * G, t);
+    }
+    lds_barrier();  // B: W' tile and the next X tile are visible
+
+    // ---- phase 3: lane = sample; acc += w'ᵀ·[x | w'] on the registers of phase 1
+    {
+      const float4 w4 = *reinterpret_cast<const float4*>(sWn + lane * K);
+      if (wave == NWAVE - 1) {  // columns 81..83 of [X | W'] (its xv[18..20] were Hᵀ padding)
+        xv[NC - 3] = w4.x;
+        xv[NC - 2] = w4.y;
+        xv[NC - 1] = w4.z;
+      }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        acc[c][0] = fmaf(w4.x, xv[c], acc[c][0]);
+        acc[c][1] = fmaf(w4.y, xv[c], acc[c][1]);
+        acc[c][2] = fmaf(w4.z, xv[c], acc[c][2]);
+        acc[c][3] = fmaf(w4.w, xv[c], acc[c][3]);
+      }
+      acc33 = fmaf(w4.w, w4.w, acc33);
+    }
+  }
+
+  // ---- end of launch: DPP tree over each 16-lane row, row sums via LDS, fp64 partial row
+  lds_barrier();  // the X region becomes the row-sum scratch
+  float* red = reinterpret_cast<float*>(smem + L_X);
+  float* myred = red + (wave * 4 + (lane >> 4)) * NR;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      float r = acc[c][j];
+      r = dpp_add<0xB1>(r);   // quad_perm [1,0,3,2]
+      r = dpp_add<0x4E>(r);   // quad_perm [2,3,0,1]
+      r = dpp_add<0x141>(r);  // row_half_mirror
+      r = dpp_add<0x140>(r);  // row_mirror: every lane holds its row's sum
+      if ((lane & 15) == 0) myred[c * K + j] = r;
+    }
+  {
+    float r = acc33;
+    r = dpp_add<0xB1>(r);
+    r = dpp_add<0x4E>(r);
+    r = dpp_add<0x141>(r);
+    r = dpp_add<0x140>(r);
+    if ((lane & 15) == 0) myred[NC * K] = r;
+  }
+  lds_barrier();
+  double* prow = partials + (size_t)blockIdx.x * (K * V);
+  for (int e = t; e < K * V; e += NT) {
+    const int j = e / V;
+    const int v = e - j * V;
+    const int w = v < 3 * NF ? v / NF : 3;
+    int idx;  // position inside wave w's row sums
+    if (v < V - 1) idx = (v - NF * w) * K + j;
+    else idx = j < K - 1 ? (NC - 3 + j) * K + (K - 1) : NC * K;  // column 84 = B[.][3] = B[3][.]
+    const float* rr = red + (w * 4) * NR + idx;
+    prow[e] = ((double)rr[0] + (double)rr[NR]) + ((double)rr[2 * NR] + (double)rr[3 * NR]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Basis update (one workgroup): the k×F epilogue, all in fp64.
 // ------------------------------------------------------------------------------------------------
 __host__ __device__ inline size_t update_lds_doubles(int F, int k, int KP) {
@@ -1014,7 +1252,20 @@ static bool pick_mfma(int x_dtype, int F, int k, PassKernel* out) {
 static int padded_k(int k) { return k <= 4 ? 4 : (k <= 8 ? 8 : 16); }
 
 static constexpr size_t kMaxLds = 160 * 1024;
-static bool g_force_valu = getenv("CNMF_FORCE_VALU") != nullptr;  // A/B switch for benchmarking
+// A/B switches for benchmarking: CNMF_PASS_KERNEL=valu|mfma|sl restricts the accumulating pass to
+// one kernel family (CNMF_FORCE_VALU=1 is the older spelling of "valu")
+static const char* pass_choice() {
+  const char* e = getenv("CNMF_PASS_KERNEL");
+  if (e && *e) return e;
+  return getenv("CNMF_FORCE_VALU") ? "valu" : "";
+}
+static bool g_force_valu = strcmp(pass_choice(), "valu") == 0;
+static bool g_no_sl = strcmp(pass_choice(), "valu") == 0 || strcmp(pass_choice(), "mfma") == 0;
+
+// the sample-lane pass serves the headline shape: fp32 X, F = 81, k = 4 (full tiles)
+static bool use_sl(int x_dtype, int F, int k) {
+  return !g_no_sl && x_dtype == CNMF_F32 && F == sl::F && k == sl::K;
+}
 
 static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds, bool mfma_ok = true) {
   if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
@@ -1102,13 +1353,36 @@ int cnmf_padded_k(int k) { return (k < 1 || k > 16) ? -1 : padded_k(k); }
 
 int64_t cnmf_stage_doubles(int n_out) { return (int64_t)NSLICE * (n_out > 0 ? n_out : 1); }
 
+// Grid of the accumulating pass.  For the sample-lane pass: its workgroups over the full tiles plus
+// one workgroup of mu_pass_kernel for a ragged tail (its partial row is the last one).
+static int64_t sl_grid(int64_t n_rows, int64_t* n_full, bool* tail) {
+  *n_full = n_rows / TS;
+  *tail = (n_rows % TS) != 0;
+  int64_t g = 0;
+  if (*n_full > 0) {
+    g = pass_grid(*n_full * TS, reinterpret_cast<PassFn>(&mu_pass_sl_kernel), sl::L_TOTAL);
+    if (g < 0) return -1;
+  }
+  return g;
+}
+
+static int64_t main_grid(int64_t n_rows, int x_dtype, int F, int k, PassKernel* pk, size_t* lds) {
+  if (use_sl(x_dtype, F, k)) {
+    int64_t n_full;
+    bool tail;
+    const int64_t g = sl_grid(n_rows, &n_full, &tail);
+    return g < 0 ? -1 : g + (tail ? 1 : 0);
+  }
+  return pass_grid(n_rows, pk->fn, *lds);
+}
+
 int64_t cnmf_pass_blocks(int64_t n_rows, int n_features, int k, int x_dtype) {
   if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
   PassKernel pk;
   size_t lds = 0;
   int st = select_pass(x_dtype, n_features, k, &pk, &lds);
   if (st) return st;
-  int64_t nb = pass_grid(n_rows, pk.fn, lds);
+  int64_t nb = main_grid(n_rows, x_dtype, n_features, k, &pk, &lds);
   if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed (no HIP device?)");
   return nb;
 }
@@ -1132,19 +1406,45 @@ int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, c
   size_t lmain = 0;
   int st = select_pass(x_dtype, n_features, k, &pmain, &lmain);
   if (st) return st;
-  const int64_t nb = pass_grid(n_rows, pmain.fn, lmain);
+  const int64_t nb = main_grid(n_rows, x_dtype, n_features, k, &pmain, &lmain);
   if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (nb == 0) return CNMF_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int F = n_features;
+  const bool sl_path = use_sl(x_dtype, n_features, k);
+  if (sl_path && flags == (CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE)) {
+    int64_t n_full;
+    bool tail;
+    const int64_t g = sl_grid(n_rows, &n_full, &tail);
+    if (g > 0) {
+      hipLaunchKernelGGL(mu_pass_sl_kernel, dim3((unsigned)g), dim3(NT), sl::L_TOTAL, s,
+                         static_cast<const float*>(X), static_cast<float*>(W), Ht, HHt, partials,
+                         n_full, l1_W, l2_W);
+      HIP_CHECK(hipGetLastError());
+    }
+    if (!tail) return CNMF_OK;
+    // the ragged tail (< 64 rows) on one workgroup of the VALU pass, partial row g
+    PassKernel pk;
+    size_t lds = 0;
+    st = select_pass(x_dtype, n_features, k, &pk, &lds, false);
+    if (st) return st;
+    if (max_resident(pk.fn, lds) <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+    const void* Xt = static_cast<const float*>(X) + n_full * TS * F;
+    void* Wt = static_cast<float*>(W) + n_full * TS * k;
+    double* pt = partials + g * (int64_t)k * (F + k);
+    int64_t rows = n_rows - n_full * TS, one = 1;
+    void* args[] = {(void*)&Xt, &Wt, (void*)&Ht, (void*)&HHt, &pt, &rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&one};
+    HIP_CHECK(hipLaunchKernel(pk.fn, dim3(1), dim3(NT), args, lds, s));
+    return CNMF_OK;
+  }
   PassKernel pk = pmain;
   size_t lds = lmain;
-  if (flags & CNMF_PASS_LOSS) {
+  if ((flags & CNMF_PASS_LOSS) || sl_path) {
     st = select_pass(x_dtype, n_features, k, &pk, &lds, false);
     if (st) return st;
     if (max_resident(pk.fn, lds) <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   }
   const int64_t n_tiles = (n_rows + TS - 1) / TS;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  int F = n_features;
   void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&n_tiles};
   HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, s));
   return CNMF_OK;

@@ -36,18 +36,24 @@ def main():
     fn(buf, 1)
     n = 20
     for flags in (3, 1):
-        plan.iterate(n) if flags == 3 else [plan.sample_pass(1) for _ in range(n)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n):
+            plan.sample_pass(flags)
+        e1.record()
         torch.cuda.synchronize()
+        pass_us = e0.elapsed_time(e1) * 1e3 / n
         fn(buf, 1)
         waves = buf[8]
         tiles_per_wave = (plan.n_rows / 64) / plan.n_parts
-        out = {"flags": flags, "waves": waves, "tiles_per_wave": round(tiles_per_wave, 2)}
+        out = {"flags": flags, "waves": waves, "pass_us": round(pass_us, 2), "tiles_per_wave": round(tiles_per_wave, 2)}
         tot = 0
         for i in range(1, 7):
             cyc = buf[i] / waves / tiles_per_wave
             tot += cyc
             out[NAMES[i]] = round(cyc, 1)
         out["total_cycles_per_tile"] = round(tot, 1)
+        out["implied_GHz"] = round(tot * tiles_per_wave / (pass_us * 1e3), 3)
         print(json.dumps(out), flush=True)
 
 

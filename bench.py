@@ -81,6 +81,7 @@ def cpu_baseline(X, W0, H0, budget_s):
 
 
 def load_traffic(path, n_rows, F, k):
+    """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py)."""
     try:
         with open(path) as f:
             d = json.load(f)
@@ -90,7 +91,8 @@ def load_traffic(path, n_rows, F, k):
     ent = d.get(key)
     if not ent:
         return None, None
-    return ent.get("hbm_bytes_per_launch"), ent.get("source")
+    per_it = ent.get("hbm_bytes_per_iteration", ent.get("hbm_bytes_per_launch"))
+    return per_it, ent.get("source")
 
 
 def main():
@@ -130,7 +132,8 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * K)]
+    persistent = world == 1 and plan.persistent
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if persistent else 2 * K)]
     stream = torch.cuda.current_stream(dev)
     for e in events:  # creates the HIP events (outside the timed region)
         e.record(stream)
@@ -156,8 +159,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    pass_ms = [events[2 * i].elapsed_time(events[2 * i + 1]) for i in range(K)]
-    avg_pass_s = float(np.mean(pass_ms)) / 1e3
+    plan.check_sync_error()
+    if persistent:  # ONE launch ran all K iterations (pass + in-launch reduction + basis update)
+        launches = 1
+        avg_launch_s = events[0].elapsed_time(events[1]) / 1e3
+    else:
+        launches = K
+        avg_launch_s = float(np.mean([events[2 * i].elapsed_time(events[2 * i + 1])
+                                      for i in range(K)])) / 1e3
+    avg_pass_s = avg_launch_s
 
     el_t = torch.tensor([elapsed, avg_pass_s], dtype=torch.float64, device=dev)
     if world > 1:
@@ -167,7 +177,9 @@ def main():
     sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
     sw = 8 if args.dtype == "f64" else 4
     bytes_per_pass = n_rows * (F * sx + 2 * k * sw)
-    achieved = bytes_per_pass / avg_pass_s / 1e9
+    iters_per_launch = K if persistent else 1
+    bytes_per_launch = bytes_per_pass * iters_per_launch
+    achieved = bytes_per_launch / avg_pass_s / 1e9
 
     # sanity of the measured state (cheap): the objective is finite, W/H non-negative
     err = plan.frobenius_error()
@@ -179,11 +191,18 @@ def main():
         return
 
     traffic, traffic_src = load_traffic(args.traffic_json, n_rows, F, k)
-    roofline = {"bound": "hbm", "kernel": "mu_pass_kernel", "achieved": round(achieved, 1),
+    if traffic is not None:
+        traffic = traffic * iters_per_launch
+    kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
+             "update per launch)" if persistent else "sample pass (mu_pass_sl_kernel / mu_pass_kernel)")
+    roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": bytes_per_pass,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_iteration": bytes_per_pass,
+                "launches_timed": launches, "iterations_per_launch": iters_per_launch,
                 "avg_launch_us": round(avg_pass_s * 1e6, 2),
+                "avg_us_per_iteration_in_launch": round(avg_pass_s / iters_per_launch * 1e6, 2),
                 "max_over_ranks_avg_launch_us": round(avg_pass_s_max * 1e6, 2)}
 
     cpu = None

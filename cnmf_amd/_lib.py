@@ -56,7 +56,10 @@ _SIGS = {
                                   _vp, _vp]),
     "cnmf_hbm_probe": (_i32, [_vp, _i64, _vp, _i32, _vp]),
     "cnmf_mu_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
-                                  _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp]),
+                                  _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _vp]),
+    "cnmf_counter_words": (_i64, []),
+    "cnmf_counter_err_word": (_i32, []),
+    "cnmf_mu_persistent": (_i32, [_i64, _i32, _i32, _i32]),
 }
 
 

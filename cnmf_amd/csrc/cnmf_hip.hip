@@ -817,6 +817,129 @@ __device__ __forceinline__ void lds_barrier() {
 }
 }  // namespace sl
 
+namespace sl {
+// ---- the three phases of one tile (shared by mu_pass_sl_kernel and mu_iter_sl_kernel)
+
+// phase 1: lane = sample, wave = 21 features: xv[] <- x[lane][21w..21w+20], partial num -> sP
+__device__ __forceinline__ void phase1(unsigned char* smem, float (&xv)[NC], int wave, int lane) {
+  const float* sX = reinterpret_cast<const float*>(smem + L_X);
+  const float* sHt = reinterpret_cast<const float*>(smem + L_HT);
+  double* sP = reinterpret_cast<double*>(smem + L_P);
+  const int fbase = NF * wave;
+  const float* xr = sX + lane * F + fbase;
+#pragma unroll
+  for (int c = 0; c < NF; ++c) xv[c] = xr[c];
+  double p[K] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int c0 = 0; c0 < NF; c0 += 7) {
+    float pc[K] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = c0; c < c0 + 7; ++c) {
+      const float4 h = *reinterpret_cast<const float4*>(sHt + (fbase + c) * K);
+      pc[0] = fmaf(xv[c], h.x, pc[0]);
+      pc[1] = fmaf(xv[c], h.y, pc[1]);
+      pc[2] = fmaf(xv[c], h.z, pc[2]);
+      pc[3] = fmaf(xv[c], h.w, pc[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) p[j] += (double)pc[j];
+  }
+  double* pw = sP + ((size_t)wave * TS + lane) * K;
+  *reinterpret_cast<double2*>(pw) = make_double2(p[0], p[1]);
+  *reinterpret_cast<double2*>(pw + 2) = make_double2(p[2], p[3]);
+}
+
+// phase 2: lane = (sample 16w + lane/4, component lane%4): the MU update of w[s][j] in fp64
+__device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ W, int64_t tile, int wpar,
+                                       int wave, int lane, double l1, double l2) {
+  const double* sP = reinterpret_cast<const double*>(smem + L_P);
+  const double* sHHt = reinterpret_cast<const double*>(smem + L_HHT);
+  float* sWn = reinterpret_cast<float*>(smem + L_WN);
+  const int s = 16 * wave + (lane >> 2);
+  const int j = lane & 3;
+  const double num = (sP[(0 * TS + s) * K + j] + sP[(1 * TS + s) * K + j]) +
+                     (sP[(2 * TS + s) * K + j] + sP[(3 * TS + s) * K + j]);
+  const float* sWo = reinterpret_cast<const float*>(smem + L_W + wpar * WB);
+  const float4 wv = *reinterpret_cast<const float4*>(sWo + s * K);
+  const double wold = (double)sWo[s * K + j];
+  const double* hr = sHHt + j * K;
+  double den = 0.0;
+  den = fma((double)wv.x, hr[0], den);
+  den = fma((double)wv.y, hr[1], den);
+  den = fma((double)wv.z, hr[2], den);
+  den = fma((double)wv.w, hr[3], den);
+  if (l1 > 0.0) den += l1;              // SK:616-617
+  if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
+  if (den == 0.0) den = EPS32;          // SK:620
+  const float wn = (float)(wold * (num / den));  // SK:622-629
+  W[((size_t)tile * TS + s) * K + j] = wn;
+  sWn[s * K + j] = wn;
+}
+
+// phase 3: lane = sample; acc += w'ᵀ·[x | w'] on the registers of phase 1 (SK:639-640)
+__device__ __forceinline__ void phase3(const unsigned char* smem, float (&xv)[NC], float (&acc)[NC][K],
+                                       float& acc33, int wave, int lane) {
+  const float* sWn = reinterpret_cast<const float*>(smem + L_WN);
+  const float4 w4 = *reinterpret_cast<const float4*>(sWn + lane * K);
+  if (wave == NWAVE - 1) {  // columns 81..83 of [X | W'] (its xv[18..20] were Hᵀ padding)
+    xv[NC - 3] = w4.x;
+    xv[NC - 2] = w4.y;
+    xv[NC - 1] = w4.z;
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    acc[c][0] = fmaf(w4.x, xv[c], acc[c][0]);
+    acc[c][1] = fmaf(w4.y, xv[c], acc[c][1]);
+    acc[c][2] = fmaf(w4.z, xv[c], acc[c][2]);
+    acc[c][3] = fmaf(w4.w, xv[c], acc[c][3]);
+  }
+  acc33 = fmaf(w4.w, w4.w, acc33);
+}
+
+// The workgroup's accumulators -> its fp64 partial row [K][V]: a DPP tree over each 16-lane row,
+// the 4 row sums of each wave through LDS (`red`, NWAVE*4*NR floats), the 4 waves summed in fp64.
+// SC1: store the row write-through (an in-launch hand-off, MI355X_MICROARCH.md valid-forms table).
+template <bool SC1>
+__device__ __forceinline__ void flush_acc(float* red, float (&acc)[NC][K], float& acc33, double* prow,
+                                          int wave, int lane, int t) {
+  float* myred = red + (wave * 4 + (lane >> 4)) * NR;
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      float r = acc[c][j];
+      r = dpp_add<0xB1>(r);   // quad_perm [1,0,3,2]
+      r = dpp_add<0x4E>(r);   // quad_perm [2,3,0,1]
+      r = dpp_add<0x141>(r);  // row_half_mirror
+      r = dpp_add<0x140>(r);  // row_mirror: every lane holds its row's sum
+      if ((lane & 15) == 0) myred[c * K + j] = r;
+    }
+  {
+    float r = acc33;
+    r = dpp_add<0xB1>(r);
+    r = dpp_add<0x4E>(r);
+    r = dpp_add<0x141>(r);
+    r = dpp_add<0x140>(r);
+    if ((lane & 15) == 0) myred[NC * K] = r;
+  }
+  lds_barrier();
+  for (int e = t; e < K * V; e += NT) {
+    const int j = e / V;
+    const int v = e - j * V;
+    const int w = v < 3 * NF ? v / NF : 3;
+    int idx;  // position inside wave w's row sums
+    if (v < V - 1) idx = (v - NF * w) * K + j;
+    else idx = j < K - 1 ? (NC - 3 + j) * K + (K - 1) : NC * K;  // column 84 = B[.][3] = B[3][.]
+    const float* rr = red + (w * 4) * NR + idx;
+    const double val = ((double)rr[0] + (double)rr[NR]) + ((double)rr[2 * NR] + (double)rr[3 * NR]);
+    if (SC1)
+      __hip_atomic_store(prow + e, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      prow[e] = val;
+  }
+}
+}  // namespace sl
+
 __global__ __launch_bounds__(NT, 3) void mu_pass_sl_kernel(const float* __restrict__ X,
                                                           float* __restrict__ W,
                                                           const double* __restrict__ Ht,
@@ -1072,6 +1195,343 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   basis_update_block(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats,
                      reinterpret_cast<double*>(smem));
+}
+
+// ------------------------------------------------------------------------------------------------
+// The persistent multi-iteration kernel for the headline shape (F = 81, k = 4, fp32, full tiles):
+// n_iter complete MU iterations (SK:831-870 for a tol == 0 stretch) in ONE launch.
+//
+// Each workgroup keeps the SAME tiles every iteration (static round-robin) and runs the sample-lane
+// tile pipeline of mu_pass_sl_kernel over them.  At the end of an iteration its fp64 partial row
+// [K][V] is published write-through (sc1) and the cross-block reduction runs in-launch:
+//   * groups of <= 32 workgroups (g = block % NG): the last arriver of a group (its ticket value
+//     says so) sums the members' rows in member order and publishes the group row;
+//   * the last arriving group combiner sums the NG group rows in group order -> AB = [WᵀX | WᵀW]
+//     (deterministic: no order depends on arrival) and raises the iteration flag;
+//   * every workgroup polls that flag (one lane, sc1 loads, s_sleep, bounded by a timeout that sets
+//     an error word instead of hanging), reads AB (sc1) and applies the basis update itself, in
+//     fp64 in LDS (SK:634-728; bit-identical arithmetic to basis_update_block), so H never makes
+//     another round trip.
+// Hand-off protocol: MI355X_MICROARCH.md "valid forms" table row 1 (sc1 stores, every storing wave
+// `s_waitcnt vmcnt(0)`, a barrier, ONE lane's agent-scope add / flag store; sc1 loads by the
+// consumer after its poll matched, the other waves behind a barrier).
+// While the tail of the reduction runs, the first two tiles of the next iteration are already in
+// LDS / in flight, so HBM keeps streaming across the iteration boundary.
+// Residency: launched cooperatively (the runtime checks grid <= co-resident capacity).
+// Counters (caller-owned, zero at rest): the last combiner of the launch zeroes them again.
+// ------------------------------------------------------------------------------------------------
+namespace sl {
+constexpr int L_RED = L_TOTAL;                          // flush scratch [NWAVE*4][NR] fp32
+constexpr int L_H = L_RED + (RED + 15) / 16 * 16;       // H fp64 [K][F]
+constexpr int L_AB = L_H + K * F * 8;                   // AB fp64 [K][V]
+constexpr int L_FLAG = L_AB + K * V * 8;                // 4 ints
+constexpr int L_PTOTAL = L_FLAG + 16;
+constexpr int GROUP = 32;                               // workgroups per first-level group
+constexpr int MAX_GROUPS = 64;
+constexpr uint64_t SPIN_TIMEOUT = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
+}  // namespace sl
+
+// counter words (uint32): [0] reduce_kernel's ticket; the persistent kernel's at 128-byte strides
+constexpr int CNT_GROUP0 = 32;
+constexpr int CNT_TOP = CNT_GROUP0 + 32 * sl::MAX_GROUPS;
+constexpr int CNT_FLAG = CNT_TOP + 32;
+constexpr int CNT_ERR = CNT_FLAG + 32;
+constexpr int CNT_WORDS = CNT_ERR + 32;
+
+// sHt (fp32 [84][4], rows >= 81 zero) and sHHt (fp64 [4][4]) from the fp64 H in LDS; the HHᵀ
+// arithmetic (lanes over f, fixed shuffle tree) is that of basis_update_block.
+__device__ __forceinline__ void sl_derive_basis(unsigned char* smem, int t) {
+  using namespace sl;
+  const double* sH = reinterpret_cast<const double*>(smem + L_H);
+  float* sHt = reinterpret_cast<float*>(smem + L_HT);
+  double* sHHt = reinterpret_cast<double*>(smem + L_HHT);
+  for (int e = t; e < NWAVE * NF * K; e += NT) {
+    const int f = e / K;
+    const int j = e - f * K;
+    sHt[e] = f < F ? (float)sH[j * F + f] : 0.f;
+  }
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  for (int e = wave; e < K * K; e += NWAVE) {
+    const int j = e / K;
+    const int m = e - j * K;
+    double v = 0.0;
+    for (int f = lane; f < F; f += 64) v = fma(sH[j * F + f], sH[m * F + f], v);
+    v = wave_sum(v);
+    if (lane == 0) sHHt[e] = v;
+  }
+  __syncthreads();
+}
+
+// H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728)
+__device__ __forceinline__ void sl_update_basis(unsigned char* smem, int t, double l1, double l2) {
+  using namespace sl;
+  double* sH = reinterpret_cast<double*>(smem + L_H);
+  const double* sAB = reinterpret_cast<const double*>(smem + L_AB);
+  double hn[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int e = t + NT * u;
+    hn[u] = 0.0;
+    if (e < K * F) {
+      const int j = e / F;
+      const int f = e - j * F;
+      double h = sH[e];
+      const double num = sAB[j * V + f];                                 // (WᵀX)[j][f], SK:639
+      double den = 0.0;                                                  // ((WᵀW)·H)[j][f], SK:640
+      for (int m = 0; m < K; ++m) den = fma(sAB[j * V + F + m], sH[m * F + f], den);
+      if (l1 > 0.0) den += l1;                                           // SK:702-703
+      if (l2 > 0.0) den = den + l2 * h;                                  // SK:704-705
+      if (den == 0.0) den = EPS32;                                       // SK:706
+      hn[u] = h * (num / den);                                           // SK:722-726
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (t + NT * u < K * F) sH[t + NT * u] = hn[u];
+  __syncthreads();
+  sl_derive_basis(smem, t);
+}
+
+struct PersistArgs {
+  const float* X;
+  float* W;
+  double* H64;       // in: the basis; out: the final basis
+  double* Ht;        // out [F][4]
+  double* HHt;       // out [4][4]
+  double* partials;  // [G][K*V] per-workgroup rows
+  double* groups;    // [NG][K*V] group rows
+  double* AB;        // [K*V]: in (apply_first) / out (the last iteration's reduced accumulators)
+  uint32_t* cnt;     // CNT_WORDS counters
+  int64_t n_tiles;
+  int n_iter;
+  int n_groups;
+  double l1W, l2W, l1H, l2H;
+  int apply_first;   // first apply the pending basis update from AB (multi-GPU: AB all-reduced)
+  int apply_last;    // apply the last iteration's basis update in-launch (single GPU)
+};
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// out[o] = Σ_m rows[m][o] in m order for the rows m = m0, m0 + step, ... (cnt rows); sc1 loads
+__device__ __forceinline__ void sum_rows_sc1(const double* rows, int m0, int step, int cnt, double* lds_out,
+                                             double* g_out, int t) {
+  using namespace sl;
+  constexpr int n_out = K * V;
+  for (int o = t; o < n_out; o += NT) {
+    double v = 0.0;
+    int m = 0;
+    for (; m + 8 <= cnt; m += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = ld_sc1(rows + (size_t)(m0 + (m + u) * step) * n_out + o);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v += x[u];
+    }
+    for (; m < cnt; ++m) v += ld_sc1(rows + (size_t)(m0 + m * step) * n_out + o);
+    if (lds_out) lds_out[o] = v;
+    st_sc1(g_out + o, v);
+  }
+}
+
+// PD = register tile sets in flight (1: three workgroups per CU in 168 VGPRs; 2: two workgroups per
+// CU in 256 VGPRs with two tiles in flight each).  At tile q the staged tile q+1 leaves its register
+// set, which is immediately refilled with tile q+1+PD.
+#ifdef CNMF_STAMPS
+// diagnostic timeline of the persistent kernel (s_memrealtime, 100 MHz): per iteration and
+// workgroup [0] = rows published (arrival), [1] = next iteration's basis ready (resume); per
+// iteration the top combiner's AB publish time.  Never in the product build.
+constexpr int TL_IT = 64, TL_WG = 2048;
+__device__ unsigned long long g_tl[TL_IT * TL_WG * 2];
+__device__ unsigned long long g_tl_pub[TL_IT];
+__device__ unsigned long long g_tl_start[TL_WG];
+#define TL(it_, slot_)                                                                          \
+  do {                                                                                          \
+    if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define TL_PUB(it_) do { if (t == 0 && (it_) < TL_IT) g_tl_pub[it_] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_START do { if (t == 0 && b < TL_WG) g_tl_start[b] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define TL(it_, slot_) do {} while (0)
+#define TL_PUB(it_) do {} while (0)
+#define TL_START do {} while (0)
+#endif
+
+template <int PD>
+__global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(PersistArgs a) {
+  using namespace sl;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int b = blockIdx.x;
+  const int G = gridDim.x;
+  const int NG = a.n_groups;
+  const int g = b % NG;                          // group members: g, g + NG, g + 2 NG, ...
+  const int gs = (G - g + NG - 1) / NG;
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
+  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.W);
+  double* sH = reinterpret_cast<double*>(smem + L_H);
+  double* sAB = reinterpret_cast<double*>(smem + L_AB);
+  int* sFlag = reinterpret_cast<int*>(smem + L_FLAG);
+  uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
+  uint32_t* cnt_top = a.cnt + CNT_TOP;
+  uint32_t* flag = a.cnt + CNT_FLAG;
+  uint32_t* err = a.cnt + CNT_ERR;
+
+  // ---- the basis for the first iteration
+  for (int e = t; e < K * F; e += NT) sH[e] = a.H64[e];
+  if (a.apply_first)
+    for (int e = t; e < K * V; e += NT) sAB[e] = a.AB[e];
+  if (t < 4) reinterpret_cast<float*>(smem + L_X + XB)[t] = 0.f;
+  __syncthreads();
+  if (a.apply_first)
+    sl_update_basis(smem, t, a.l1H, a.l2H);
+  else
+    sl_derive_basis(smem, t);
+
+  float acc[NC][K];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[c][j] = 0.f;
+  float acc33 = 0.f;
+
+  // tiles of this workgroup: b + G·i, i < nbt, the same every iteration.  The host guarantees
+  // nbt >= PD + 2, so a tile's W was stored at least one tile before it is prefetched again.
+  const int nbt = (int)((a.n_tiles - b + G - 1) / G);
+  const int total = a.n_iter * nbt;
+  auto tile_at = [&](int q) -> int64_t { return b + (int64_t)G * (q % nbt); };
+  u32x4 pfA[PFN], pfB[PFN];
+  sl_prefetch(pfA, Xb, Wb, tile_at(0), t);
+  if (PD == 2 && total > 1) sl_prefetch(pfB, Xb, Wb, tile_at(1), t);
+  sl_stage(smem, 0, pfA, t);
+  if (total > PD) sl_prefetch(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
+  lds_barrier();
+  TL_START;
+
+  bool alive = true;
+  int wpar = 0;
+  auto body = [&](int q, u32x4 (&pf)[PFN]) {
+    const int it = q / nbt;
+    const int i = q - it * nbt;
+    const bool end_it = i + 1 == nbt;
+    const bool last_it = it + 1 == a.n_iter;
+    const bool has1 = q + 1 < total;
+    const bool hasP = q + 1 + PD < total;
+    const int64_t tile = tile_at(q);
+    float xv[NC];
+    phase1(smem, xv, wave, lane);
+    // this wave's W store of the previous tile has landed (vmcnt retires in order; at most the 6
+    // loads issued after it may remain) before any wave passes barrier A and prefetches W again
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    lds_barrier();  // A
+    phase2(smem, a.W, tile, wpar, wave, lane, a.l1W, a.l2W);
+    if (has1) sl_stage(smem, wpar ^ 1, pf, t);
+    if (hasP && !end_it) sl_prefetch(pf, Xb, Wb, tile_at(q + 1 + PD), t);
+    lds_barrier();  // B
+    phase3(smem, xv, acc, acc33, wave, lane);
+    wpar ^= 1;
+    if (!end_it) return;
+
+    // ---- end of the iteration: publish this workgroup's row, then the in-launch reduction
+    flush_acc<true>(reinterpret_cast<float*>(smem + L_RED), acc, acc33, a.partials + (size_t)b * (K * V),
+                    wave, lane, t);
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+#pragma unroll
+      for (int j = 0; j < K; ++j) acc[c][j] = 0.f;
+    acc33 = 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
+    __syncthreads();
+    if (hasP) sl_prefetch(pf, Xb, Wb, tile_at(q + 1 + PD), t);  // in flight during the reduction
+    TL(it, 0);
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
+      sFlag[1] = 0;
+      sFlag[2] = 1;
+    }
+    __syncthreads();
+    if (sFlag[0]) {  // group combiner
+      sum_rows_sc1(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * (K * V), t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
+      }
+      __syncthreads();
+      if (sFlag[1]) {  // top combiner: AB
+        sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0 && !last_it)
+          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TL_PUB(it);
+      }
+    }
+    const bool top = sFlag[1] != 0;
+    if (last_it) {
+      alive = false;
+      if (!top) return;
+      // the last combiner of the launch: every other workgroup has arrived for the last time
+      if (a.apply_last) sl_update_basis(smem, t, a.l1H, a.l2H);
+      for (int e = t; e < K * F; e += NT) a.H64[e] = sH[e];
+      for (int e = t; e < F * K; e += NT) {
+        const int f = e / K;
+        const int j = e - f * K;
+        a.Ht[e] = sH[j * F + f];
+      }
+      if (t < K * K) a.HHt[t] = reinterpret_cast<const double*>(smem + L_HHT)[t];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
+        alive = false;
+        return;
+      }
+      for (int e = t; e < K * V; e += NT) sAB[e] = ld_sc1(a.AB + e);
+      __syncthreads();
+    }
+    sl_update_basis(smem, t, a.l1H, a.l2H);
+    TL(it, 1);
+  };
+
+  for (int q = 0; q < total && alive; q += 2) {
+    if (PD == 1) body(q, pfA);
+    else body(q, pfB);
+    if (q + 1 < total && alive) body(q + 1, pfA);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1345,7 +1805,7 @@ using namespace cnmf;
 
 extern "C" {
 
-int cnmf_abi_version(void) { return 200; }
+int cnmf_abi_version(void) { return 201; }
 
 const char* cnmf_last_error(void) { return g_err; }
 
@@ -1515,6 +1975,13 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
 }
 
 #ifdef CNMF_STAMPS
+// timeline of the last persistent launch: out = [TL_IT*TL_WG*2 | TL_IT | TL_WG] u64
+int cnmf_debug_timeline(unsigned long long* host_out) {
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl), sizeof(unsigned long long) * TL_IT * TL_WG * 2));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2, HIP_SYMBOL(g_tl_pub), sizeof(unsigned long long) * TL_IT));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2 + TL_IT, HIP_SYMBOL(g_tl_start), sizeof(unsigned long long) * TL_WG));
+  return CNMF_OK;
+}
 int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
   if (reset) {
@@ -1536,18 +2003,100 @@ int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, vo
   return CNMF_OK;
 }
 
+// The persistent path serves fp32 X at F = 81, k = 4 with whole tiles and >= 3 tiles per workgroup
+// (CNMF_PERSIST=0 disables it for A/B timing).  Returns its grid, 0 when not eligible, < 0 on error.
+static bool g_no_persist = getenv("CNMF_PERSIST") && strcmp(getenv("CNMF_PERSIST"), "0") == 0;
+// prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2)
+static int g_persist_pd = (getenv("CNMF_PERSIST_PD") && atoi(getenv("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
+static PassFn persist_fn() {
+  return g_persist_pd == 1 ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1>)
+                           : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2>);
+}
+
+static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k) {
+  if (g_no_persist || !use_sl(x_dtype, F, k) || n_rows % TS != 0) return 0;
+  const int64_t n_tiles = n_rows / TS;
+  const int min_tiles = g_persist_pd + 2;  // per workgroup (the W re-read hazard, see the kernel)
+  if (n_tiles < min_tiles) return 0;
+  const int64_t maxb = max_resident(persist_fn(), sl::L_PTOTAL);
+  if (maxb <= 0) return -1;
+  int64_t n_full;
+  bool tail;
+  const int64_t rows_cap = sl_grid(n_rows, &n_full, &tail);  // = cnmf_pass_blocks: partial rows
+  if (rows_cap <= 0) return rows_cap < 0 ? -1 : 0;
+  int64_t G = std::min<int64_t>({maxb, rows_cap, n_tiles / min_tiles, (int64_t)sl::GROUP * sl::MAX_GROUPS});
+  const int64_t rounds = (n_tiles + G - 1) / G;
+  return (n_tiles + rounds - 1) / rounds;  // <= G, so every workgroup still owns >= min_tiles
+}
+
+int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
+  const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
+  return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
+}
+
+int64_t cnmf_counter_words(void) { return CNT_WORDS; }
+int cnmf_counter_err_word(void) { return CNT_ERR; }
+
+// one cooperative launch of mu_iter_sl_kernel
+static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, double* H64, double* Ht,
+                             double* HHt, double* partials, int64_t n_parts, double* stage,
+                             uint32_t* counter, double* AB, int64_t n_rows, double l1_W, double l2_W,
+                             double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s) {
+  if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
+                                  (long long)n_parts, (long long)G);
+  PersistArgs pa;
+  pa.X = static_cast<const float*>(X);
+  pa.W = static_cast<float*>(W);
+  pa.H64 = H64;
+  pa.Ht = Ht;
+  pa.HHt = HHt;
+  pa.partials = partials;
+  pa.groups = stage;
+  pa.AB = AB;
+  pa.cnt = counter;
+  pa.n_tiles = n_rows / TS;
+  pa.n_iter = n_iter;
+  pa.n_groups = (int)((G + sl::GROUP - 1) / sl::GROUP);
+  pa.l1W = l1_W;
+  pa.l2W = l2_W;
+  pa.l1H = l1_H;
+  pa.l2H = l2_H;
+  pa.apply_first = apply_first;
+  pa.apply_last = apply_last;
+  void* args[] = {&pa};
+  HIP_CHECK(hipLaunchCooperativeKernel(persist_fn(), dim3((unsigned)G),
+                                       dim3(NT), args, sl::L_PTOTAL, s));
+  return CNMF_OK;
+}
+
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
-                       void* const* pass_events, void* stream) {
+                       void* const* events, int n_events, void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (n_iter <= 0) return CNMF_OK;
+  const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
+  if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (G > 0) {
+    if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB)
+      return set_err(CNMF_ERR_ARG, "null pointer argument");
+    if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+      return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+    if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+    int st = launch_persistent(G, n_iter, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB,
+                               n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs);
+    if (st) return st;
+    if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+    return CNMF_OK;
+  }
+  const bool ev = events && n_events >= 2 * n_iter;
   for (int it = 0; it < n_iter; ++it) {
-    if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it]), hs));
+    if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it]), hs));
     int st = cnmf_mu_sample_pass(X, x_dtype, W, Ht, HHt, partials, n_rows, n_features, k, l1_W,
                                  l2_W, CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE, stream);
     if (st) return st;
-    if (pass_events) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(pass_events[2 * it + 1]), hs));
+    if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it + 1]), hs));
     st = cnmf_reduce_update(partials, n_parts, stage, counter, AB, H64, Ht, HHt, n_features, k, l1_H,
                             l2_H, stats, stream);
     if (st) return st;

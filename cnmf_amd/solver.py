@@ -30,15 +30,13 @@ def _ptr(t: torch.Tensor | None):
     return None if t is None else t.data_ptr()
 
 
-def _event_array(events, n_iter):
+def _event_array(events):
     if events is None:
-        return None
-    if len(events) != 2 * n_iter:
-        raise ValueError("pass_events must hold 2*n_iter events")
+        return None, 0
     handles = [int(e.cuda_event) for e in events]
     if not all(handles):
         raise ValueError("record each event once before passing it (creates the HIP event)")
-    return (ctypes.c_void_p * len(handles))(*handles)
+    return (ctypes.c_void_p * len(handles))(*handles), len(handles)
 
 
 class MUPlan:
@@ -81,7 +79,11 @@ class MUPlan:
         self.HHt = torch.zeros((KP, KP), dtype=f64, device=dev)
         self.partials = torch.zeros((max(self.n_parts, 1), self.n_out), dtype=f64, device=dev)
         self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out)), dtype=f64, device=dev)
-        self.counter = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.counter = torch.zeros(int(self.lib.cnmf_counter_words()), dtype=torch.int32, device=dev)
+        self.err_word = int(self.lib.cnmf_counter_err_word())
+        with torch.cuda.device(self.device):
+            p = self.lib.cnmf_mu_persistent(self.n_rows, self.F, self.k, self.xdt)
+        self.persistent = bool(check(p, "cnmf_mu_persistent")) and self.world == 1
         self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)
@@ -128,10 +130,18 @@ class MUPlan:
         if self.world > 1:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
+    def check_sync_error(self):
+        """Raise if a persistent launch gave up waiting for a workgroup (its results are invalid);
+        synchronises the stream."""
+        if getattr(self, "persistent", False) and int(self.counter[self.err_word].item()) != 0:
+            self.counter[self.err_word] = 0
+            raise _lib.HipLibraryError("persistent MU launch timed out waiting for a workgroup "
+                                       "(grid not co-resident?); results of that launch are invalid")
+
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
         """n_iter MU iterations (SK:831-870) without host synchronisation.  pass_events: optional
-        list of 2*n_iter recorded-once torch.cuda.Event(enable_timing=True) bracketing each pass
-        (single GPU only)."""
+        recorded-once torch.cuda.Event(enable_timing=True) list (single GPU only): 2 events around
+        the one launch when self.persistent, else 2*n_iter events around each sample pass."""
         if n_iter <= 0:
             return
         if not update_H:
@@ -144,7 +154,7 @@ class MUPlan:
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
                     _ptr(self.counter), _ptr(self.AB), None, self.n_rows, self.F, self.k,
-                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _event_array(pass_events, n_iter),
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, *_event_array(pass_events),
                     self._stream()), "cnmf_mu_iterations")
             return
         for _ in range(n_iter):
@@ -178,6 +188,8 @@ def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool 
         stop = min(max_iter, (it // 10 + 1) * 10) if tol > 0 else max_iter
         plan.iterate(stop - it, update_H)
         it = stop
+        if tol > 0 or it >= max_iter:
+            plan.check_sync_error()
         if tol > 0 and it % 10 == 0:  # SK:872-884
             error = plan.frobenius_error()
             errors.append((it, error))

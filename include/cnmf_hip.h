@@ -94,15 +94,29 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
                        double* AB, double* H64, double* Ht, double* HHt, int n_features, int k,
                        double l1_H, double l2_H, double* stats, void* stream);
 
-/* n_iter single-GPU MU iterations (pass + reduce_update each) launched back to back with no host
- * synchronisation: the body of SK:831-870 for tol == 0 stretches.  pass_events (may be NULL):
- * 2*n_iter caller-created hipEvent_t recorded on `stream` right before / after each sample pass
- * (live per-launch timing of the dominant kernel for the roofline report). */
+/* Words of the caller-owned uint32 counter buffer (zeroed once at allocation; every launch leaves
+ * it zeroed again except the error word) and the index of its error word: non-zero after a
+ * persistent launch gave up waiting for a workgroup (the results of that launch are invalid). */
+int64_t cnmf_counter_words(void);
+int cnmf_counter_err_word(void);
+
+/* 1 when cnmf_mu_iterations runs this shape as ONE persistent launch (mu_iter_sl_kernel: fp32 X,
+ * F = 81, k = 4, n_rows a multiple of 64 and >= 192), 0 when it launches pass + reduce per
+ * iteration. */
+int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
+
+/* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
+ * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction
+ * and the basis update in-launch (stage then holds the group rows, counter: cnmf_counter_words()).
+ * Other shapes: pass + reduce_update per iteration.
+ * events (may be NULL), caller-created hipEvent_t recorded on `stream` for live kernel timing:
+ *   persistent: events[0] / events[1] before / after the launch (n_events >= 2);
+ *   otherwise : events[2i] / events[2i+1] around sample pass i (n_events >= 2*n_iter). */
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
-                       void* const* pass_events, void* stream);
+                       void* const* events, int n_events, void* stream);
 
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */

@@ -1,0 +1,85 @@
+"""Timeline of the persistent MU launch from the diagnostic stamps build (s_memrealtime, 100 MHz).
+
+    python -m cnmf_amd.build --stamps
+    CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_stamps.so python tools/timeline_persist.py [--iters 20]
+
+Per steady-state iteration: the streaming span of each workgroup (basis ready -> rows published),
+the arrival skew (first -> last workgroup), the reduction tail (last arrival -> AB published) and
+the resume latency (AB published -> basis ready in each workgroup).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+TL_IT, TL_WG = 64, 2048
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    import torch
+    from cnmf_amd import _lib
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(a.rows, 81, seed=0, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    lib = _lib.load()
+    fn = lib.cnmf_debug_timeline
+    fn.argtypes = [ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    plan = MUPlan(torch.from_numpy(X).cuda(), 4)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    assert plan.persistent
+    plan.iterate(5)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    plan.iterate(a.iters)
+    e1.record()
+    torch.cuda.synchronize()
+    launch_us = e0.elapsed_time(e1) * 1e3
+    buf = np.zeros(TL_IT * TL_WG * 2 + TL_IT + TL_WG, dtype=np.uint64)
+    _lib.check(fn(buf.ctypes.data), "timeline")
+    G = plan.n_parts
+    from cnmf_amd.solver import MUPlan as _M  # noqa: F401
+    tl = buf[:TL_IT * TL_WG * 2].reshape(TL_IT, TL_WG, 2).astype(np.int64)
+    pub = buf[TL_IT * TL_WG * 2:TL_IT * TL_WG * 2 + TL_IT].astype(np.int64)
+    start = buf[TL_IT * TL_WG * 2 + TL_IT:].astype(np.int64)
+    # the grid actually launched: workgroups with a start stamp in this launch
+    g = int(np.count_nonzero(start[:G] >= start[:G].max() - 10_000_000))
+    n = min(a.iters, TL_IT)
+    arr = tl[:n, :g, 0]
+    res = tl[:n, :g, 1]
+    t0 = start[:g].min()
+    rows = []
+    for it in range(1, n - 1):
+        span = (arr[it] - res[it - 1]) * 10 / 1e3  # us
+        rows.append({
+            "it": it,
+            "period_us": (pub[it] - pub[it - 1]) * 10 / 1e3,
+            "stream_med_us": float(np.median(span)), "stream_min_us": float(span.min()),
+            "stream_max_us": float(span.max()),
+            "skew_us": (arr[it].max() - arr[it].min()) * 10 / 1e3,
+            "tail_us": (pub[it] - arr[it].max()) * 10 / 1e3,
+            "resume_med_us": float(np.median(res[it] - pub[it])) * 10 / 1e3,
+            "resume_max_us": float((res[it] - pub[it]).max()) * 10 / 1e3,
+        })
+    summary = {k: round(float(np.median([r[k] for r in rows])), 2) for k in rows[0] if k != "it"}
+    summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
+                    "us_per_iter": round(launch_us / a.iters, 2),
+                    "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})
+    print(json.dumps(summary), flush=True)
+    for r in rows[:5]:
+        print(json.dumps({k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

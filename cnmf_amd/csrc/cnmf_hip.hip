@@ -1204,7 +1204,7 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
 // Each workgroup keeps the SAME tiles every iteration (static round-robin) and runs the sample-lane
 // tile pipeline of mu_pass_sl_kernel over them.  At the end of an iteration its fp64 partial row
 // [K][V] is published write-through (sc1) and the cross-block reduction runs in-launch:
-//   * groups of <= 32 workgroups (g = block % NG): the last arriver of a group (its ticket value
+//   * groups of <= 16 workgroups (g = block % NG): the last arriver of a group (its ticket value
 //     says so) sums the members' rows in member order and publishes the group row;
 //   * the last arriving group combiner sums the NG group rows in group order -> AB = [WᵀX | WᵀW]
 //     (deterministic: no order depends on arrival) and raises the iteration flag;
@@ -1226,12 +1226,13 @@ constexpr int L_H = L_RED + (RED + 15) / 16 * 16;       // H fp64 [K][F]
 constexpr int L_AB = L_H + K * F * 8;                   // AB fp64 [K][V]
 constexpr int L_FLAG = L_AB + K * V * 8;                // 4 ints
 constexpr int L_PTOTAL = L_FLAG + 16;
-constexpr int GROUP = 32;                               // workgroups per first-level group
+constexpr int GROUP = 16;                               // workgroups per first-level group
 constexpr int MAX_GROUPS = 64;
 constexpr uint64_t SPIN_TIMEOUT = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
 }  // namespace sl
 
 // counter words (uint32): [0] reduce_kernel's ticket; the persistent kernel's at 128-byte strides
+static_assert(sl::MAX_GROUPS <= NSLICE, "group rows live in the reduction stage buffer");
 constexpr int CNT_GROUP0 = 32;
 constexpr int CNT_TOP = CNT_GROUP0 + 32 * sl::MAX_GROUPS;
 constexpr int CNT_FLAG = CNT_TOP + 32;
@@ -1319,30 +1320,40 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// out[o] = Σ_m rows[m][o] in m order for the rows m = m0, m0 + step, ... (cnt rows); sc1 loads
+// out[o] = Σ_m rows[m][o] in m order for the rows m = m0, m0 + step, ... (cnt rows); sc1 loads.
+// Batches of 16 rows for both of a thread's outputs are issued before any is summed (row index
+// clamped and the extra terms dropped after the load, so no load sits behind a branch).
 __device__ __forceinline__ void sum_rows_sc1(const double* rows, int m0, int step, int cnt, double* lds_out,
                                              double* g_out, int t) {
   using namespace sl;
   constexpr int n_out = K * V;
-  for (int o = t; o < n_out; o += NT) {
-    double v = 0.0;
-    int m = 0;
-    for (; m + 8 <= cnt; m += 8) {
-      double x[8];
+  constexpr int RB = 16;
+  static_assert(n_out <= 2 * NT, "two outputs per thread");
+  const int o0 = t;
+  const int o1 = t + NT < n_out ? t + NT : t;
+  double v0 = 0.0, v1 = 0.0;
+  for (int m = 0; m < cnt; m += RB) {
+    double x0[RB], x1[RB];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = ld_sc1(rows + (size_t)(m0 + (m + u) * step) * n_out + o);
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v += x[u];
+    for (int u = 0; u < RB; ++u) {
+      const int r = m0 + min(m + u, cnt - 1) * step;
+      x0[u] = ld_sc1(rows + (size_t)r * n_out + o0);
+      x1[u] = ld_sc1(rows + (size_t)r * n_out + o1);
     }
-    for (; m < cnt; ++m) v += ld_sc1(rows + (size_t)(m0 + m * step) * n_out + o);
-    if (lds_out) lds_out[o] = v;
-    st_sc1(g_out + o, v);
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      v0 += m + u < cnt ? x0[u] : 0.0;
+      v1 += m + u < cnt ? x1[u] : 0.0;
+    }
+  }
+  if (lds_out) lds_out[o0] = v0;
+  st_sc1(g_out + o0, v0);
+  if (t + NT < n_out) {
+    if (lds_out) lds_out[o1] = v1;
+    st_sc1(g_out + o1, v1);
   }
 }
 
-// PD = register tile sets in flight (1: three workgroups per CU in 168 VGPRs; 2: two workgroups per
-// CU in 256 VGPRs with two tiles in flight each).  At tile q the staged tile q+1 leaves its register
-// set, which is immediately refilled with tile q+1+PD.
 #ifdef CNMF_STAMPS
 // diagnostic timeline of the persistent kernel (s_memrealtime, 100 MHz): per iteration and
 // workgroup [0] = rows published (arrival), [1] = next iteration's basis ready (resume); per

@@ -73,6 +73,17 @@ def main():
             "resume_max_us": float((res[it] - pub[it]).max()) * 10 / 1e3,
         })
     summary = {k: round(float(np.median([r[k] for r in rows])), 2) for k in rows[0] if k != "it"}
+    # is the skew systematic?  per-workgroup stream time, iterations 1..n-2
+    spans = np.stack([(arr[it] - res[it - 1]) * 10 / 1e3 for it in range(1, n - 1)])  # [it][wg]
+    mean_wg = spans.mean(axis=0)
+    half = spans.shape[0] // 2
+    corr = float(np.corrcoef(spans[:half].mean(axis=0), spans[half:].mean(axis=0))[0, 1])
+    nbt = np.array([(plan.n_rows // 64 - b + g - 1) // g for b in range(g)])
+    by_xcd = [round(float(mean_wg[np.arange(g) % 8 == x].mean()), 2) for x in range(8)]
+    summary.update({"wg_stream_corr_between_halves": round(corr, 3), "stream_by_b_mod_8": by_xcd,
+                    "stream_by_tiles": {int(v): round(float(mean_wg[nbt == v].mean()), 2) for v in np.unique(nbt)},
+                    "per_wg_mean_min_max": [round(float(mean_wg.min()), 2), round(float(mean_wg.max()), 2)],
+                    "within_wg_std_us": round(float(spans.std(axis=0).mean()), 2)})
     summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
                     "us_per_iter": round(launch_us / a.iters, 2),
                     "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})

@@ -143,17 +143,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if world == 1:
-        plan.iterate(K, pass_events=events)
-    else:
-        from cnmf_amd import _lib
-        for i in range(K):
-            events[2 * i].record(stream)
-            plan.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
-            events[2 * i + 1].record(stream)
-            plan.reduce(plan.n_out, plan.AB)
-            plan._allreduce(plan.AB)
-            plan.basis_update()
+    plan.iterate(K, pass_events=events)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -193,8 +183,14 @@ def main():
     traffic, traffic_src = load_traffic(args.traffic_json, n_rows, F, k)
     if traffic is not None:
         traffic = traffic * iters_per_launch
-    kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
-             "update per launch)" if persistent else "sample pass (mu_pass_sl_kernel / mu_pass_kernel)")
+    if persistent:
+        kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
+                 "update per launch)")
+    elif plan.persistent_shape:
+        kname = ("mu_iter_sl_kernel shard step (one iteration per launch: pending basis update, "
+                 "pass, in-launch reduction; all_reduce between launches)")
+    else:
+        kname = "sample pass (mu_pass_kernel / mu_pass_mfma_kernel)"
     roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,

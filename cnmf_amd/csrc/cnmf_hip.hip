@@ -1217,7 +1217,7 @@ __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __re
 // consumer after its poll matched, the other waves behind a barrier).
 // While the tail of the reduction runs, the first two tiles of the next iteration are already in
 // LDS / in flight, so HBM keeps streaming across the iteration boundary.
-// Residency: launched cooperatively (the runtime checks grid <= co-resident capacity).
+// Residency: grid <= the occupancy query's co-resident capacity; every spin is bounded (error word).
 // Counters (caller-owned, zero at rest): the last combiner of the launch zeroes them again.
 // ------------------------------------------------------------------------------------------------
 namespace sl {
@@ -2075,9 +2075,65 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
   void* args[] = {&pa};
-  HIP_CHECK(hipLaunchCooperativeKernel(persist_fn(), dim3((unsigned)G),
-                                       dim3(NT), args, sl::L_PTOTAL, s));
+  // a plain launch: the grid is at most the occupancy query's co-resident capacity (persist_grid;
+  // 106 SGPRs admit 6 workgroups per CU by MI355X_MICROARCH.md's residency formula, we use 2) and
+  // every wait in the kernel is bounded, so a short residency ends in the error word, not a hang.
+  // (hipLaunchCooperativeKernel made rocprofv3 crash at process exit and costs ~17 us per launch.)
+  HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, s));
   return CNMF_OK;
+}
+
+int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                       double* partials, int64_t n_parts, double* stage, uint32_t* counter, double* AB,
+                       int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
+                       double l2_H, int apply_first, void* stream) {
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (!X || !W || !H64 || !Ht || !HHt || !stage || !counter || !AB)
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
+  if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (G > 0) {
+    // one launch of the persistent kernel with n_iter = 1: its in-launch reduction only takes
+    // tickets (no workgroup ever waits), so a plain launch is safe at any residency
+    if (!partials) return set_err(CNMF_ERR_ARG, "null pointer argument");
+    if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+      return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+    if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold too few rows");
+    PersistArgs pa;
+    pa.X = static_cast<const float*>(X);
+    pa.W = static_cast<float*>(W);
+    pa.H64 = H64;
+    pa.Ht = Ht;
+    pa.HHt = HHt;
+    pa.partials = partials;
+    pa.groups = stage;
+    pa.AB = AB;
+    pa.cnt = counter;
+    pa.n_tiles = n_rows / TS;
+    pa.n_iter = 1;
+    pa.n_groups = (int)((G + sl::GROUP - 1) / sl::GROUP);
+    pa.l1W = l1_W;
+    pa.l2W = l2_W;
+    pa.l1H = l1_H;
+    pa.l2H = l2_H;
+    pa.apply_first = apply_first;
+    pa.apply_last = 0;
+    void* args[] = {&pa};
+    HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, hs));
+    return CNMF_OK;
+  }
+  int st;
+  if (apply_first) {
+    st = cnmf_basis_update(AB, H64, Ht, HHt, n_features, k, l1_H, l2_H, 1, nullptr, stream);
+    if (st) return st;
+  }
+  st = cnmf_mu_sample_pass(X, x_dtype, W, Ht, HHt, partials, n_rows, n_features, k, l1_W, l2_W,
+                           CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE, stream);
+  if (st) return st;
+  const int64_t nb = cnmf_pass_blocks(n_rows, n_features, k, x_dtype);
+  if (nb < 0) return (int)nb;
+  if (nb == 0) return CNMF_OK;
+  return cnmf_reduce_partials(partials, nb, k * (n_features + k), stage, counter, AB, stream);
 }
 
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,

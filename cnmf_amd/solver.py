@@ -83,7 +83,8 @@ class MUPlan:
         self.err_word = int(self.lib.cnmf_counter_err_word())
         with torch.cuda.device(self.device):
             p = self.lib.cnmf_mu_persistent(self.n_rows, self.F, self.k, self.xdt)
-        self.persistent = bool(check(p, "cnmf_mu_persistent")) and self.world == 1
+        self.persistent_shape = bool(check(p, "cnmf_mu_persistent"))  # the persistent kernel serves it
+        self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
         self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)
@@ -126,6 +127,14 @@ class MUPlan:
                                              _ptr(self.HHt), self.F, self.k, self.l1_H, self.l2_H, 1,
                                              None, self._stream()), "cnmf_basis_update")
 
+    def shard_step(self, apply_first: bool):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_mu_shard_step(
+                _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
+                _ptr(self.AB), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H,
+                self.l2_H, int(apply_first), self._stream()), "cnmf_mu_shard_step")
+
     def _allreduce(self, t: torch.Tensor):
         if self.world > 1:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
@@ -157,11 +166,18 @@ class MUPlan:
                     self.l1_W, self.l2_W, self.l1_H, self.l2_H, *_event_array(pass_events),
                     self._stream()), "cnmf_mu_iterations")
             return
-        for _ in range(n_iter):
-            self.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
-            self.reduce(self.n_out, self.AB)
+        # multi-GPU: per iteration ONE shard step (pending basis update from the all-reduced AB,
+        # then this shard's W update and local [WᵀX | WᵀW] into AB) and ONE all_reduce of AB
+        ev = list(pass_events) if pass_events is not None else None
+        stream = torch.cuda.current_stream(self.device) if ev is not None else None
+        for i in range(n_iter):
+            if ev is not None:
+                ev[2 * i].record(stream)
+            self.shard_step(apply_first=i > 0)
+            if ev is not None:
+                ev[2 * i + 1].record(stream)
             self._allreduce(self.AB)
-            self.basis_update()
+        self.basis_update()
 
     def frobenius_error(self) -> float:
         """sqrt(‖X − W·H‖²) over all ranks (SK:85-129 with square_root=True); synchronises."""

@@ -118,6 +118,18 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
                        void* const* events, int n_events, void* stream);
 
+/* One MU iteration of a row shard for the multi-GPU driver (SK:831-870 with the accumulators
+ * all-reduced between ranks):
+ *   apply_first = 1: first the pending basis update from AB (= the all-reduced [WᵀX | WᵀW] of the
+ *                    previous iteration; SK:634-728), refreshing H64 / Ht / HHt;
+ *   then the W update of this shard (SK:526-631) and this shard's reduced [WᵀX | WᵀW] into AB.
+ * The caller all-reduces AB (RCCL) and passes apply_first = 1 next time; cnmf_basis_update applies
+ * the last pending update.  Persistent shapes run as ONE launch of the persistent kernel. */
+int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                       double* partials, int64_t n_parts, double* stage, uint32_t* counter, double* AB,
+                       int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
+                       double l2_H, int apply_first, void* stream);
+
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);

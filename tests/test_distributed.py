@@ -1,9 +1,10 @@
 """World-size-2 gloo test of the row-sharded MU orchestration on CPU.
 
-The multi-GPU host path (`MUPlan.iterate` / `run_mu` with world > 1: per-rank pass -> reduce ->
-all_reduce(AB) -> identical basis update; the loss check all-reduces one double) runs unchanged;
-only the three device launches are replaced by a NumPy stand-in (test-only: the product has no CPU
-path).  Two ranks on disjoint row shards must reproduce the unsharded oracle fit.
+The multi-GPU host path (`MUPlan.iterate` / `run_mu` with world > 1: per iteration one shard step
+(pending basis update from the all-reduced AB, then the shard's W update and local [WᵀX | WᵀW])
+and one all_reduce(AB); a final basis update; the loss check all-reduces one double) runs
+unchanged; only the device launches are replaced by a NumPy stand-in (test-only: the product has
+no CPU path).  Two ranks on disjoint row shards must reproduce the unsharded oracle fit.
 """
 import os
 import socket
@@ -52,6 +53,12 @@ class _NumpyPlan(MUPlan):
 
     def reduce(self, n_out, out):
         out.copy_(torch.from_numpy(self._partial[:n_out]))
+
+    def shard_step(self, apply_first):  # the contract of cnmf_mu_shard_step
+        if apply_first:
+            self.basis_update()
+        self.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+        self.reduce(self.n_out, self.AB)
 
     def basis_update(self):
         AB = self.AB.numpy().reshape(self.k, self.V)

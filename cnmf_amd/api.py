@@ -150,7 +150,8 @@ def _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio):
 # the core fit
 # ------------------------------------------------------------------------------------------------
 def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
-                   l1_ratio, random_state, verbose, device, group=None, return_plan=False):
+                   l1_ratio, random_state, verbose, device, group=None, return_plan=False,
+                   normalise=None):
     """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
     torch = _torch()
     from .solver import MUPlan, run_mu
@@ -216,6 +217,8 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
     if n_iter == max_iter and tol > 0:
         warnings.warn("Maximum number of iterations %d reached. Increase it to improve "
                       "convergence." % max_iter, ConvergenceWarning)
+    if normalise is not None and update_H:
+        plan.normalise(normalise)  # §8 a6: unit-norm basis rows, scales folded into W
     Wd, Hd = plan.W, plan.H()
     if return_plan:
         return Wd, Hd, n_iter, plan, as_torch, X
@@ -230,16 +233,27 @@ def _out(t, as_torch, X):
 
 def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
               beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
-              l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None):
+              l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None,
+              normalise=None):
     """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
     `sklearn.decomposition.non_negative_factorization` (SK:905-1131), except solver defaults to
     (and must be) 'mu'.  `device` selects the HIP device (default: current).
+    `normalise` ('l1' | 'l2' | 'max' | None, default None = sklearn's output): after the fit, every
+    row of H is scaled to unit norm and the scale folded into W's column (W·H unchanged;
+    SURVEY.md §8 a6).
     """
     _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
+    _validate_normalise(normalise)
     return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
-                          l1_ratio, random_state, verbose, device)
+                          l1_ratio, random_state, verbose, device, normalise=normalise)
+
+
+def _validate_normalise(normalise):
+    if normalise not in (None, "l1", "l2", "max"):
+        raise ValueError(f"The 'normalise' parameter must be a str among {{'l1', 'l2', 'max'}} or "
+                         f"None. Got {normalise!r} instead.")
 
 
 fit = factorise
@@ -255,8 +269,9 @@ class NMF:
 
     def __init__(self, n_components="auto", *, init=None, solver="mu", beta_loss="frobenius",
                  tol=1e-4, max_iter=200, random_state=None, alpha_W=0.0, alpha_H="same",
-                 l1_ratio=0.0, verbose=0, shuffle=False, device=None):
+                 l1_ratio=0.0, verbose=0, shuffle=False, device=None, normalise=None):
         self.n_components = n_components
+        self.normalise = normalise
         self.init = init
         self.solver = solver
         self.beta_loss = beta_loss
@@ -273,7 +288,8 @@ class NMF:
     def get_params(self, deep=True):
         return {k: getattr(self, k) for k in ("n_components", "init", "solver", "beta_loss", "tol",
                                               "max_iter", "random_state", "alpha_W", "alpha_H",
-                                              "l1_ratio", "verbose", "shuffle", "device")}
+                                              "l1_ratio", "verbose", "shuffle", "device",
+                                              "normalise")}
 
     def set_params(self, **params):
         for k, v in params.items():
@@ -283,6 +299,7 @@ class NMF:
     def _validate(self):
         _validate_params(self.n_components, self.init, self.solver, self.beta_loss, self.tol,
                          self.max_iter, self.alpha_W, self.alpha_H, self.l1_ratio)
+        _validate_normalise(self.normalise)
 
     def fit_transform(self, X, y=None, W=None, H=None):
         """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H."""
@@ -290,7 +307,7 @@ class NMF:
         Wd, Hd, n_iter, plan, as_torch, Xc = _fit_transform(
             X, W, H, self.n_components, self.init, True, self.tol, self.max_iter, self.alpha_W,
             self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
-            return_plan=True)
+            return_plan=True, normalise=self.normalise)
         self.reconstruction_err_ = plan.frobenius_error()
         self.n_components_ = int(Hd.shape[0])
         self.components_ = _out(Hd, as_torch, Xc)

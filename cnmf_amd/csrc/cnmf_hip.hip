@@ -1546,6 +1546,56 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
 }
 
 // ------------------------------------------------------------------------------------------------
+// Normalisation projection (build spec, no sklearn counterpart): every basis row
+// H_j is rescaled to unit norm and the scale folded into column j of W, so W·H is unchanged:
+//   s_j = ‖H_j‖ (norm 1: L1, 2: L2, 3: max), H_j <- H_j / s_j, W[:, j] <- W[:, j]·s_j
+// (rows with s_j == 0 are left alone, s_j := 1).  One workgroup computes s (fp64, fixed-order wave
+// sums), rewrites H64 and derives Ht / HHt; then a grid-stride pass scales W.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(RED_NT) void normalise_basis_kernel(double* __restrict__ H64,
+                                                                 double* __restrict__ Ht,
+                                                                 double* __restrict__ HHt,
+                                                                 double* __restrict__ scale, int F,
+                                                                 int k, int KP, int norm) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* ss = reinterpret_cast<double*>(smem);  // [16] scales
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  for (int j = wave; j < k; j += RED_NT / 64) {
+    double v = 0.0;
+    for (int f = lane; f < F; f += 64) {
+      const double h = H64[j * F + f];
+      if (norm == 1) v += fabs(h);
+      else if (norm == 2) v = fma(h, h, v);
+      else v = fmax(v, fabs(h));
+    }
+    if (norm == 3) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    } else {
+      v = wave_sum(v);
+    }
+    if (norm == 2) v = sqrt(v);
+    if (lane == 0) ss[j] = v > 0.0 ? v : 1.0;
+  }
+  __syncthreads();
+  if (t < k) scale[t] = ss[t];
+  for (int e = t; e < k * F; e += RED_NT) H64[e] = H64[e] / ss[e / F];
+  __syncthreads();  // workgroup-scope fence + barrier: the H64 stores are visible to this workgroup
+  basis_update_block(nullptr, H64, Ht, HHt, F, k, KP, 0.0, 0.0, 0, nullptr,
+                     reinterpret_cast<double*>(smem) + 16);
+}
+
+template <typename TC>
+__global__ __launch_bounds__(256) void scale_columns_kernel(TC* __restrict__ W, const double* __restrict__ scale,
+                                                            int64_t n, int k) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride)
+    W[e] = (TC)((double)W[e] * scale[e % k]);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Deterministic fp64 reduction of partials[n_parts][n_out]; optional fused basis update.
 // grid = (ceil(n_out/64), nslice): block (c, s) sums rows of slice s for 64 outputs (<= 8 rows per
 // thread, one batch of independent loads) and writes one stage row write-through (sc1); one lane
@@ -1971,6 +2021,37 @@ int cnmf_basis_update(const double* AB, double* H64, double* Ht, double* HHt, in
   hipLaunchKernelGGL(basis_update_kernel, dim3(1), dim3(RED_NT), lds,
                      reinterpret_cast<hipStream_t>(stream), AB, H64, Ht, HHt, n_features, k, KP, l1_H,
                      l2_H, do_update, stats);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_normalise(void* W, int w_dtype, double* H64, double* Ht, double* HHt, double* scale,
+                   int64_t n_rows, int n_features, int k, int norm, void* stream) {
+  int st = check_update_args(H64, Ht, HHt, n_features, k);
+  if (st) return st;
+  if (!scale || (n_rows > 0 && !W)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (norm < 1 || norm > 3) return set_err(CNMF_ERR_ARG, "norm must be 1 (L1), 2 (L2) or 3 (max)");
+  if (w_dtype != CNMF_F32 && w_dtype != CNMF_F64) return set_err(CNMF_ERR_ARG, "W must be f32 or f64");
+  if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const int KP = padded_k(k);
+  const size_t lds = (16 + update_lds_doubles(n_features, k, KP)) * sizeof(double);
+  if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the update kernel");
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&normalise_basis_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(normalise_basis_kernel, dim3(1), dim3(RED_NT), lds, hs, H64, Ht, HHt, scale,
+                     n_features, k, KP, norm);
+  HIP_CHECK(hipGetLastError());
+  const int64_t n = n_rows * k;
+  if (n == 0) return CNMF_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>(4096, (n + 255) / 256);
+  if (w_dtype == CNMF_F32)
+    hipLaunchKernelGGL(scale_columns_kernel<float>, dim3(blocks), dim3(256), 0, hs, static_cast<float*>(W),
+                       scale, n, k);
+  else
+    hipLaunchKernelGGL(scale_columns_kernel<double>, dim3(blocks), dim3(256), 0, hs, static_cast<double*>(W),
+                       scale, n, k);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }

@@ -179,6 +179,21 @@ class MUPlan:
             self._allreduce(self.AB)
         self.basis_update()
 
+    _NORMS = {"l1": 1, "l2": 2, "max": 3}
+
+    def normalise(self, norm: str = "l2") -> torch.Tensor:
+        """Normalisation projection: unit-norm basis rows, scales folded into W's
+        columns (W·H unchanged).  Returns the k scales (fp64, on the device)."""
+        if norm not in self._NORMS:
+            raise ValueError(f"normalise must be one of {sorted(self._NORMS)} or None, got {norm!r}")
+        scale = torch.empty(self.k, dtype=torch.float64, device=self.device)
+        wdt = _lib.F64 if self.tc == torch.float64 else _lib.F32
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_normalise(_ptr(self.W), wdt, _ptr(self.H64), _ptr(self.Ht),
+                                          _ptr(self.HHt), _ptr(scale), self.n_rows, self.F, self.k,
+                                          self._NORMS[norm], self._stream()), "cnmf_normalise")
+        return scale
+
     def frobenius_error(self) -> float:
         """sqrt(‖X − W·H‖²) over all ranks (SK:85-129 with square_root=True); synchronises."""
         self.sample_pass(_lib.PASS_LOSS)

@@ -130,6 +130,13 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
                        int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
                        double l2_H, int apply_first, void* stream);
 
+/* Normalisation projection (no sklearn counterpart, off unless asked for):
+ *   s_j = ‖H_j‖ (norm 1 = L1, 2 = L2, 3 = max; s_j := 1 for an all-zero row),
+ *   H_j <- H_j / s_j (H64, and Ht / HHt refreshed), W[:, j] <- W[:, j]·s_j, scale[j] = s_j,
+ * so W·H is unchanged.  W: [n_rows][k] of w_dtype (CNMF_F32 or CNMF_F64); scale: k doubles. */
+int cnmf_normalise(void* W, int w_dtype, double* H64, double* Ht, double* HHt, double* scale,
+                   int64_t n_rows, int n_features, int k, int norm, void* stream);
+
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);

@@ -158,3 +158,20 @@ def update_h_from_accumulators(A, B, H, l1_reg_H=0.0, l2_reg_H=0.0):
         denominator = denominator + l2_reg_H * H
     denominator[denominator == 0] = EPSILON
     return H * (A / denominator)
+
+
+def normalise(W, H, norm="l2"):
+    """Normalisation projection (build spec, no sklearn function): unit-norm rows
+    of H with the scales folded into the columns of W, so W @ H is unchanged.  All-zero rows keep
+    scale 1.  Returns (W', H', s)."""
+    H = np.asarray(H, dtype=np.float64)
+    if norm == "l1":
+        s = np.abs(H).sum(axis=1)
+    elif norm == "l2":
+        s = np.sqrt((H * H).sum(axis=1))
+    elif norm == "max":
+        s = np.abs(H).max(axis=1)
+    else:
+        raise ValueError(norm)
+    s = np.where(s > 0, s, 1.0)
+    return np.asarray(W, dtype=np.float64) * s[None, :], H / s[:, None], s

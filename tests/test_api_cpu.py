@@ -29,6 +29,7 @@ def test_drop_in_name_reexports():
     (dict(l1_ratio=2.0), "'l1_ratio' parameter"),
     (dict(init="bogus"), "'init' parameter"),
     (dict(n_components=0), "'n_components' parameter"),
+    (dict(normalise="l3"), "'normalise' parameter"),
 ])
 def test_invalid_params(X, kw, msg):
     with pytest.raises(ValueError, match=msg):

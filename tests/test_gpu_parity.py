@@ -172,3 +172,44 @@ def test_full_size_properties():
         outs.append((plan.W.clone(), plan.H64.clone()))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     assert bool((outs[0][0] >= 0).all()) and bool((outs[0][1] >= 0).all())
+
+
+@pytest.mark.parametrize("norm", ["l1", "l2", "max"])
+@pytest.mark.parametrize("dt", ["float32", "float64"])
+def test_normalise_projection(norm, dt):
+    """§8 a6: unit-norm basis rows, scales folded into W (W·H unchanged), vs the oracle."""
+    import torch
+    from cnmf_amd.solver import MUPlan
+    rng = np.random.default_rng(8)
+    N, F, k = 3001, 81, 5
+    X = rng.random((N, F)).astype(dt)
+    W0 = rng.random((N, k)).astype(dt)
+    H0 = (rng.random((k, F)) * 3).astype(dt)
+    H0[2] = 0.0  # an all-zero basis row keeps scale 1
+    plan = MUPlan(torch.from_numpy(X).cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    s = plan.normalise(norm).cpu().numpy()
+    Wr, Hr, sr = mu_ref.normalise(W0, H0, norm)
+    np.testing.assert_allclose(s, sr, rtol=1e-14)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    assert rel_fro(H, Hr) < 1e-15
+    assert rel_fro(W, Wr) < (1e-7 if dt == "float32" else 1e-15)
+    np.testing.assert_allclose(plan.HHt.cpu().numpy()[:k, :k], H @ H.T, rtol=1e-13, atol=1e-15)
+    err = plan.frobenius_error()  # Ht/HHt are consistent with the new H: the loss is unchanged
+    ref = mu_ref.frobenius_error(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64))
+    assert abs(err - ref) / ref < 1e-6
+
+
+def test_factorise_normalise_option():
+    cnmf_amd = _api()
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(20_000, 81, seed=1, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom", tol=0.0,
+                                 max_iter=100, normalise="l2")
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=100, tol=0.0)
+    Wn, Hn, _ = mu_ref.normalise(Wr, Hr, "l2")
+    assert rel_fro(W, Wn) <= TOL32 and rel_fro(H, Hn) <= TOL32
+    np.testing.assert_allclose(np.linalg.norm(H.astype(np.float64), axis=1), 1.0, rtol=1e-6)

@@ -60,6 +60,10 @@ _SIGS = {
     "cnmf_counter_words": (_i64, []),
     "cnmf_counter_err_word": (_i32, []),
     "cnmf_mu_persistent": (_i32, [_i64, _i32, _i32, _i32]),
+    "cnmf_als_table_doubles": (_i32, []),
+    "cnmf_als_prepare": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _f64, _vp]),
+    "cnmf_als_sample_pass": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f64, _i32, _vp]),
+    "cnmf_als_basis_update": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64, _vp]),
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                   _i32, _f64, _f64, _f64, _f64, _i32, _vp]),

@@ -8,8 +8,10 @@ scikit-learn 1.7.2's Frobenius MU path (SK = sklearn/decomposition/_nmf.py):
   _compute_regularization       SK:1254-1265
   _initialize_nmf ('random')    SK:303-314   (nndsvd / nndsvda / nndsvdar: cnmf_amd.init)
 
-Differences, all deliberate: the only solver is 'mu' (the default here; sklearn's default 'cd'
-raises), only beta_loss='frobenius' is accepted, sparse X is not, and n_components ≤ 16.  NumPy
+Differences, all deliberate: the solvers are 'mu' (the default here; sklearn's default 'cd'
+raises) and the build's constrained ALS 'als' (sum_to_one / smoothness; k ≤ 4),
+only beta_loss='frobenius' is accepted, sparse X is not, and n_components ≤ 16.  normalise=
+('l1' | 'l2' | 'max') adds the §8 a6 projection (off by default, so 'mu' output is sklearn's).  NumPy
 inputs are copied to the GPU and results come back as NumPy arrays of X's dtype; torch tensors on a
 HIP device stay there (fp32, fp64 or bf16 X; bf16 computes in fp32 and returns fp32 W/H).
 There is no CPU fallback: without the HIP library every call raises HipLibraryError.
@@ -119,9 +121,9 @@ def _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha
     if init not in _INITS:
         raise ValueError(f"The 'init' parameter must be a str among {{'custom', 'nndsvd', "
                          f"'nndsvda', 'nndsvdar', 'random'}} or None. Got {init!r} instead.")
-    if solver != "mu":
+    if solver not in ("mu", "als"):
         raise ValueError(f"solver={solver!r} is not available: this build implements the "
-                         "multiplicative-update solver ('mu') only.")
+                         "multiplicative-update solver ('mu') and the constrained ALS ('als').")
     if beta_loss not in ("frobenius", 2, 2.0):
         raise ValueError(f"beta_loss={beta_loss!r} is not available: only 'frobenius' (2) is "
                          "implemented on the MI355X path.")
@@ -149,12 +151,26 @@ def _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio):
 # ------------------------------------------------------------------------------------------------
 # the core fit
 # ------------------------------------------------------------------------------------------------
+def _validate_als(solver, alpha_W, alpha_H, sum_to_one, smoothness):
+    if solver != "als":
+        if sum_to_one is not None or smoothness:
+            raise ValueError("sum_to_one / smoothness apply to solver='als' only")
+        return
+    if alpha_W != 0 or alpha_H not in ("same", 0, 0.0):
+        raise ValueError("solver='als' takes no alpha_W / alpha_H regularisation (use sum_to_one "
+                         "and smoothness)")
+    for name, v in (("sum_to_one", sum_to_one), ("smoothness", smoothness)):
+        if v is not None and (not isinstance(v, numbers.Real) or v < 0):
+            raise ValueError(f"The '{name}' parameter must be a float in the range [0, inf) or None. "
+                             f"Got {v!r} instead.")
+
+
 def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                    l1_ratio, random_state, verbose, device, group=None, return_plan=False,
-                   normalise=None):
+                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0):
     """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
     torch = _torch()
-    from .solver import MUPlan, run_mu
+    from .solver import ALSPlan, MUPlan, run_mu
 
     X = _check_X(X)
     as_torch = _is_torch(X)
@@ -198,12 +214,17 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
     k = int(k)
     if k > 16:
         raise ValueError(f"n_components={k} is not supported: the MI355X kernels handle 1..16.")
+    if solver == "als" and k > 4:
+        raise ValueError(f"n_components={k} is not supported by solver='als' (1..4).")
 
     regs = _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio)
     dev = torch.device(device) if device is not None else (X.device if as_torch else torch.device("cuda", torch.cuda.current_device()))
     Xd = X if as_torch else torch.from_numpy(X)
     Xd = Xd.to(dev, non_blocking=False).contiguous()
-    plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
+    if solver == "als":
+        plan = ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
+    else:
+        plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
     if W is None:  # update_H=False start: sqrt(X.mean()/k) in X's dtype (SK:1228-1232)
         if as_torch:
             avg = float(torch.sqrt(X.double().mean() / k))
@@ -234,7 +255,7 @@ def _out(t, as_torch, X):
 def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
               beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
               l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None,
-              normalise=None):
+              normalise=None, sum_to_one=None, smoothness=0.0):
     """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
@@ -243,11 +264,17 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
     `normalise` ('l1' | 'l2' | 'max' | None, default None = sklearn's output): after the fit, every
     row of H is scaled to unit norm and the scale folded into W's column (W·H unchanged;
     SURVEY.md §8 a6).
+    solver='als' selects the constrained ALS (k <= 4): per sample the exact
+    non-negative least squares with a sum-to-one penalty of weight `sum_to_one` (δ; None = off),
+    and per basis row the exact NNLS with a second-difference smoothness penalty `smoothness` (λ)
+    — see oracle/als_ref.py for the precise objective.  tol / max_iter work as for 'mu'.
     """
     _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
     _validate_normalise(normalise)
+    _validate_als(solver, alpha_W, alpha_H, sum_to_one, smoothness)
     return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
-                          l1_ratio, random_state, verbose, device, normalise=normalise)
+                          l1_ratio, random_state, verbose, device, normalise=normalise,
+                          solver=solver, sum_to_one=sum_to_one, smoothness=smoothness)
 
 
 def _validate_normalise(normalise):
@@ -269,9 +296,12 @@ class NMF:
 
     def __init__(self, n_components="auto", *, init=None, solver="mu", beta_loss="frobenius",
                  tol=1e-4, max_iter=200, random_state=None, alpha_W=0.0, alpha_H="same",
-                 l1_ratio=0.0, verbose=0, shuffle=False, device=None, normalise=None):
+                 l1_ratio=0.0, verbose=0, shuffle=False, device=None, normalise=None,
+                 sum_to_one=None, smoothness=0.0):
         self.n_components = n_components
         self.normalise = normalise
+        self.sum_to_one = sum_to_one
+        self.smoothness = smoothness
         self.init = init
         self.solver = solver
         self.beta_loss = beta_loss
@@ -289,7 +319,7 @@ class NMF:
         return {k: getattr(self, k) for k in ("n_components", "init", "solver", "beta_loss", "tol",
                                               "max_iter", "random_state", "alpha_W", "alpha_H",
                                               "l1_ratio", "verbose", "shuffle", "device",
-                                              "normalise")}
+                                              "normalise", "sum_to_one", "smoothness")}
 
     def set_params(self, **params):
         for k, v in params.items():
@@ -300,6 +330,7 @@ class NMF:
         _validate_params(self.n_components, self.init, self.solver, self.beta_loss, self.tol,
                          self.max_iter, self.alpha_W, self.alpha_H, self.l1_ratio)
         _validate_normalise(self.normalise)
+        _validate_als(self.solver, self.alpha_W, self.alpha_H, self.sum_to_one, self.smoothness)
 
     def fit_transform(self, X, y=None, W=None, H=None):
         """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H."""
@@ -307,7 +338,8 @@ class NMF:
         Wd, Hd, n_iter, plan, as_torch, Xc = _fit_transform(
             X, W, H, self.n_components, self.init, True, self.tol, self.max_iter, self.alpha_W,
             self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
-            return_plan=True, normalise=self.normalise)
+            return_plan=True, normalise=self.normalise, solver=self.solver,
+            sum_to_one=self.sum_to_one, smoothness=self.smoothness)
         self.reconstruction_err_ = plan.frobenius_error()
         self.n_components_ = int(Hd.shape[0])
         self.components_ = _out(Hd, as_torch, Xc)
@@ -331,7 +363,9 @@ class NMF:
                              f"{self.n_features_in_} features as input.")
         W, _, _ = _fit_transform(X, None, self.components_, self.n_components_, self.init, False,
                                  self.tol, self.max_iter, self.alpha_W, self.alpha_H,
-                                 self.l1_ratio, self.random_state, self.verbose, self.device)
+                                 self.l1_ratio, self.random_state, self.verbose, self.device,
+                                 solver=self.solver, sum_to_one=self.sum_to_one,
+                                 smoothness=self.smoothness)
         return W
 
     def inverse_transform(self, X=None, *, Xt=None):

@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "cnmf_hip.h"
@@ -51,6 +52,7 @@ constexpr int PF = 8;        // 16-byte chunks per thread held in registers for 
 constexpr int NSLICE = 64;   // max slices of the deterministic cross-block reduction
 constexpr int RED_NT = 256;  // threads of the reduce / update workgroups
 constexpr double EPS32 = 1.1920928955078125e-07;  // np.finfo(np.float32).eps, SK:39
+constexpr int ALS_TAB = 16 * 16 + 16;  // constrained-ALS passive-set table: 16 masks x 4x4 + valid
 
 static thread_local char g_err[512] = "";
 
@@ -113,7 +115,8 @@ struct PassLds {
 
 __host__ __device__ inline int feat_per_wave(int F) { return (F + NWAVE - 1) / NWAVE; }
 
-__host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc) {
+__host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc, size_t sh = 0) {
+  if (sh == 0) sh = sc;  // Ht element size (fp64 for the constrained-ALS pass)
   PassLds L;
   size_t xb = align16(((size_t)TS * F + 4) * sx);
   size_t rb = (size_t)NWAVE * 64 * KP * sizeof(double);
@@ -121,8 +124,8 @@ __host__ __device__ inline PassLds pass_lds(int F, int KP, size_t sx, size_t sc)
   L.w = L.region0;
   L.wn = L.w + align16((size_t)TS * KP * sc);
   L.ht = L.wn + align16((size_t)TS * KP * sc);
-  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sc);
-  L.zero = L.hht + align16((size_t)KP * KP * sizeof(double));
+  L.hht = L.ht + align16((size_t)NWAVE * feat_per_wave(F) * KP * sh);
+  L.zero = L.hht + align16((size_t)(KP == 4 ? ALS_TAB : KP * KP) * sizeof(double));
   L.total = L.zero + 16;
   return L;
 }
@@ -258,9 +261,10 @@ __device__ unsigned long long g_stamps[16];
 //            rounded once to TC, stored to HBM and to the LDS row sWn[s] (A phase input).
 //   loss   : lane sums (x − w·Ht)² over its quarter, quad-reduced into loss64 (qtr 0 lanes).
 // ------------------------------------------------------------------------------------------------
-template <typename TX, typename TC, int KP, int FT>
+template <typename TX, typename TC, int KP, int FT, bool ALS = false,
+          typename TH = typename std::conditional<ALS, double, TC>::type>
 __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __restrict__ sW,
-                                        TC* __restrict__ sWn, const TC* __restrict__ sHt,
+                                        TC* __restrict__ sWn, const TH* __restrict__ sHt,
                                         const double* __restrict__ sHHt, TC* __restrict__ W,
                                         int64_t tile, int F, int q, int k, int ns, int s_beg,
                                         int lane, bool do_loss, bool do_upd, double l1, double l2,
@@ -269,7 +273,7 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
   const int s = s_beg + (lane >> 2);
   const int fb = qtr * q;
   const TX* xr = sX + (size_t)s * F + fb;
-  const TC* hb = sHt + (size_t)fb * KP;
+  const TH* hb = sHt + (size_t)fb * KP;
   if (do_loss) {
     double w[KP];
 #pragma unroll
@@ -288,12 +292,19 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
     if (qtr == 0 && s < ns) loss64 += part;
     return;
   }
-  // fp32 (TC) FMA chains of PCH features folded into fp64 (see the precision note above)
+  // fp32 (TC) FMA chains of PCH features folded into fp64 (see the precision note above); the
+  // constrained-ALS step forms c = Hx entirely in fp64 (its solve amplifies errors by cond(Q))
   constexpr int PCH = 7;
   double p[KP];
 #pragma unroll
   for (int j = 0; j < KP; ++j) p[j] = 0.0;
-  if constexpr (FT > 0) {
+  if constexpr (ALS) {
+    for (int f = 0; f < q; ++f) {
+      const double xv = (double)to_c(xr[f]);
+#pragma unroll
+      for (int j = 0; j < KP; ++j) p[j] = fma(xv, hb[f * KP + j], p[j]);
+    }
+  } else if constexpr (FT > 0) {
     constexpr int QF = (FT + NWAVE - 1) / NWAVE;
 #pragma unroll 1
     for (int f0 = 0; f0 < QF; f0 += PCH) {
@@ -332,6 +343,62 @@ __device__ __forceinline__ void phase12(const TX* __restrict__ sX, const TC* __r
     p[j] += __shfl_xor(p[j], 2);
   }
   if (!do_upd) return;
+  if constexpr (KP == 4 && ALS) {
+    {
+      // ---- constrained-ALS W-step (oracle/als_ref.py fcls_w): w = argmin_{w>=0}
+      // ½wᵀQw - cᵀw with Q = HHᵀ + δ²11ᵀ, c = Hx + δ²1 (l1 carries δ²).  sHHt holds, per passive
+      // set (mask 0..15), T = (Q_PP)⁻¹ scattered to 4x4 and a valid flag.  Lane qtr evaluates the
+      // masks qtr, qtr+4, qtr+8, qtr+12; the least objective -½c·w among the non-negative
+      // candidates wins (ties: lowest mask), chosen across the quad by shuffles.
+      double c[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) c[j] = p[j] + l1;
+      double bestf = 1.0;
+      int bestm = 16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = qtr + 4 * u;
+        const double* T = sHHt + m * 16;
+        double w[4];
+        bool feas = sHHt[256 + m] != 0.0;
+        double f = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double v = 0.0;
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) v = fma(T[r * 4 + cc], c[cc], v);
+          w[r] = v;
+          feas = feas && v >= 0.0;
+          f = fma(c[r], v, f);
+        }
+        f *= -0.5;
+        if (feas && (f < bestf || (f == bestf && m < bestm))) {
+          bestf = f;
+          bestm = m;
+        }
+      }
+#pragma unroll
+      for (int off = 1; off <= 2; off <<= 1) {
+        const double of = __shfl_xor(bestf, off);
+        const int om = __shfl_xor(bestm, off);
+        if (of < bestf || (of == bestf && om < bestm)) {
+          bestf = of;
+          bestm = om;
+        }
+      }
+      const double* T = sHHt + min(bestm, 15) * 16;
+      double wn64 = 0.0;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) wn64 = fma(T[qtr * 4 + cc], c[cc], wn64);
+      TC wn = TC(0);
+      if (s < ns && qtr < k) {
+        wn = (TC)fmax(wn64, 0.0);
+        W[(size_t)(tile * TS + s) * k + qtr] = wn;
+      }
+      sWn[s * KP + qtr] = wn;
+      return;
+    }
+  }
   double wr[KP];
 #pragma unroll
   for (int m = 0; m < KP; ++m)
@@ -382,7 +449,7 @@ constexpr int pass_min_waves() {
                             : (KP == 8 ? (sizeof(TX) == 8 ? 2 : 3) : (sizeof(TX) == 8 ? 1 : 2)));
 }
 
-template <typename TX, int KP, int FT, int NPW, bool SPLIT>
+template <typename TX, int KP, int FT, int NPW, bool SPLIT, bool ALS = false>
 __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_kernel(const TX* __restrict__ X,
                                                      typename Compute<TX>::T* __restrict__ W,
                                                      const double* __restrict__ Ht,
@@ -391,15 +458,16 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
                                                      int F_rt, int k, double l1, double l2,
                                                      int flags, int64_t n_tiles) {
   using TC = typename Compute<TX>::T;
+  using TH = typename std::conditional<ALS, double, TC>::type;  // Ht in LDS
   constexpr bool SAME = sizeof(TX) == sizeof(TC);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int F = FT > 0 ? FT : F_rt;
   const int q = feat_per_wave(F);
-  const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC));
+  const PassLds L = pass_lds(F, KP, sizeof(TX), sizeof(TC), sizeof(TH));
   TX* sX = reinterpret_cast<TX*>(smem);
   TC* sW = reinterpret_cast<TC*>(smem + L.w);
   TC* sWn = reinterpret_cast<TC*>(smem + L.wn);
-  TC* sHt = reinterpret_cast<TC*>(smem + L.ht);
+  TH* sHt = reinterpret_cast<TH*>(smem + L.ht);
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sRed = reinterpret_cast<double*>(smem);
 
@@ -411,10 +479,10 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
   const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
   const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
-
   // basis-side constants into LDS once per launch (Ht zero-padded to 4q rows)
-  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? (TC)Ht[e] : TC(0);
-  for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
+  for (int e = t; e < NWAVE * q * KP; e += NT) sHt[e] = e < F * KP ? (TH)Ht[e] : TH(0);
+  const int n_hht = ALS ? ALS_TAB : KP * KP;  // HHt, or the ALS passive-set table
+  for (int e = t; e < n_hht; e += NT) sHHt[e] = HHt[e];
   if (t < 4) {
     sX[TS * F + t] = TX{};
     reinterpret_cast<uint32_t*>(smem + L.zero)[t] = 0u;
@@ -457,8 +525,8 @@ __global__ __launch_bounds__(NT, (pass_min_waves<TX, KP, FT>())) void mu_pass_ke
 
     // ---- phases 1+2 (wave-local, fp64)
     const int s_beg = wave * (TS / NWAVE);
-    phase12<TX, TC, KP, FT>(sX, sW, sWn, sHt, sHHt, W, tile, F, q, k, ns, s_beg, lane, do_loss, do_upd,
-                            l1, l2, loss64);
+    phase12<TX, TC, KP, FT, ALS>(sX, sW, sWn, sHt, sHHt, W, tile, F, q, k, ns, s_beg, lane, do_loss,
+                                 do_upd, l1, l2, loss64);
     STAMP(4);  // 4: phases 1+2
     if (do_upd) {
       if (SPLIT)
@@ -1596,6 +1664,220 @@ __global__ __launch_bounds__(256) void scale_columns_kernel(TC* __restrict__ W, 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Constrained ALS, basis side (the spec and its scipy-NNLS oracle:
+// oracle/als_ref.py).  One workgroup, all fp64:
+//   * H-step (do_update): one Gauss-Seidel sweep over the basis rows j = 0..k-1, each the exact
+//     NNLS  h_j = argmin_{h>=0} ½hᵀ(B_jj I + λL)h - (a_j - Σ_{m≠j} B_jm h_m)ᵀh,  L = DᵀD (second
+//     difference, pentadiagonal), by block principal pivoting (Kim & Park's BPP: swap every
+//     infeasible index, fall back to single swaps when the infeasible count stops falling), warm
+//     started from the row's current support.  The passive subsystem of a pentadiagonal matrix is
+//     pentadiagonal in the compressed index order, so each solve is an O(F) banded Cholesky
+//     (thread 0); the residuals and infeasibility tests run over all threads.
+//   * Ht / HHt from the new H (basis_update_block), then the W-step's passive-set table for
+//     Q = HHᵀ + δ²11ᵀ: per mask P (k <= 4) the inverse of Q_PP by Gauss-Jordan with partial
+//     pivoting, scattered to 4x4 (zeros outside P), and a valid flag (pivot > 1e-13·max diag).
+// ------------------------------------------------------------------------------------------------
+constexpr int ALS_MAX_F = 512;
+
+__host__ __device__ inline size_t als_lds_bytes(int F, int k) {
+  // doubles: A, H [k][F]; B [k][k]; b, x, d0, e1, e2, L0, L1, L2, z [F]; then ints: pas, inf, idx [F], 8
+  return ((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 8) * 4;
+}
+
+// M(fa, fb) of the row Hessian for |fa - fb| <= 2 (0 otherwise), fb < fa
+__device__ __forceinline__ double als_m_low(const double* e1, const double* e2, int fa, int fb) {
+  const int d = fa - fb;
+  return d == 1 ? e1[fb] : (d == 2 ? e2[fb] : 0.0);
+}
+
+__device__ double als_L_entry(int F, int a, int b) {  // (DᵀD)[a][b], b >= a, |b - a| <= 2
+  double v = 0.0;
+  for (int r = a - 2; r <= a; ++r) {
+    if (r < 0 || r > F - 3) continue;
+    const int ia = a - r, ib = b - r;
+    if (ib < 0 || ib > 2) continue;
+    const double ca = ia == 1 ? -2.0 : 1.0;
+    const double cb = ib == 1 ? -2.0 : 1.0;
+    v += ca * cb;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restrict__ AB, double* __restrict__ H64,
+                                                           double* __restrict__ Ht, double* __restrict__ HHt,
+                                                           double* __restrict__ table, int F, int k, int KP,
+                                                           double lam, double delta2, int do_update) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int V = F + k;
+  double* sA = reinterpret_cast<double*>(smem);
+  double* sH = sA + (size_t)k * F;
+  double* sB = sH + (size_t)k * F;
+  double* vb = sB + k * k;
+  double* vx = vb + F;
+  double* d0 = vx + F;
+  double* e1 = d0 + F;
+  double* e2 = e1 + F;
+  double* L0 = e2 + F;
+  double* L1 = L0 + F;
+  double* L2 = L1 + F;
+  double* vz = L2 + F;
+  int* pas = reinterpret_cast<int*>(vz + F);
+  int* inf = pas + F;
+  int* idx = inf + F;
+  int* ctl = idx + F;  // [0] n_inf, [1] max infeasible index, [2] mode, [3] n passive
+
+  if (do_update) {
+    for (int e = t; e < k * F; e += RED_NT) {
+      sA[e] = AB[(e / F) * V + (e % F)];
+      sH[e] = H64[e];
+    }
+    for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
+    __syncthreads();
+    for (int j = 0; j < k; ++j) {
+      const double bjj = sB[j * k + j];
+      if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
+      for (int f = t; f < F; f += RED_NT) {
+        double b = sA[j * F + f];
+        for (int m = 0; m < k; ++m)
+          if (m != j) b -= sB[j * k + m] * sH[m * F + f];
+        vb[f] = b;
+        d0[f] = bjj + lam * als_L_entry(F, f, f);
+        e1[f] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
+        e2[f] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
+        pas[f] = sH[j * F + f] > 0.0;
+      }
+      __syncthreads();
+      int alpha = 3, beta = F + 1;  // BPP control (thread 0's copy is the one that counts)
+      for (int iter = 0; iter < 5 * F + 10; ++iter) {
+        if (t == 0) {
+          // compress the passive set, banded Cholesky of M_PP, forward / backward substitution
+          int n = 0;
+          for (int f = 0; f < F; ++f) {
+            vx[f] = 0.0;
+            if (pas[f]) idx[n++] = f;
+          }
+          for (int a = 0; a < n; ++a) {
+            const int fa = idx[a];
+            double l2 = 0.0, l1 = 0.0;
+            if (a >= 2) l2 = als_m_low(e1, e2, fa, idx[a - 2]) / L0[a - 2];
+            if (a >= 1) l1 = (als_m_low(e1, e2, fa, idx[a - 1]) - (a >= 2 ? l2 * L1[a - 1] : 0.0)) / L0[a - 1];
+            L2[a] = l2;
+            L1[a] = l1;
+            L0[a] = sqrt(fmax(d0[fa] - l1 * l1 - l2 * l2, 1e-300));
+          }
+          for (int a = 0; a < n; ++a) {
+            double z = vb[idx[a]];
+            if (a >= 1) z -= L1[a] * vz[a - 1];
+            if (a >= 2) z -= L2[a] * vz[a - 2];
+            vz[a] = z / L0[a];
+          }
+          for (int a = n - 1; a >= 0; --a) {
+            double x = vz[a];
+            if (a + 1 < n) x -= L1[a + 1] * vz[a + 1];
+            if (a + 2 < n) x -= L2[a + 2] * vz[a + 2];
+            vz[a] = x / L0[a];  // vz now holds x in compressed order
+          }
+          for (int a = 0; a < n; ++a) vx[idx[a]] = vz[a];
+          ctl[0] = 0;
+          ctl[1] = -1;
+        }
+        __syncthreads();
+        for (int f = t; f < F; f += RED_NT) {
+          const double x = vx[f];
+          bool bad;
+          if (pas[f]) {
+            bad = x < 0.0;
+          } else {
+            double y = d0[f] * x - vb[f];
+            if (f + 1 < F) y += e1[f] * vx[f + 1];
+            if (f >= 1) y += e1[f - 1] * vx[f - 1];
+            if (f + 2 < F) y += e2[f] * vx[f + 2];
+            if (f >= 2) y += e2[f - 2] * vx[f - 2];
+            bad = y < 0.0;
+          }
+          inf[f] = bad;
+          if (bad) {
+            atomicAdd(&ctl[0], 1);
+            atomicMax(&ctl[1], f);
+          }
+        }
+        __syncthreads();
+        if (t == 0) {
+          const int ninf = ctl[0];
+          int mode;
+          if (ninf == 0) mode = 0;
+          else if (ninf < beta) { beta = ninf; alpha = 3; mode = 1; }
+          else if (alpha >= 1) { --alpha; mode = 1; }
+          else mode = 2;
+          ctl[2] = mode;
+        }
+        __syncthreads();
+        const int mode = ctl[2];
+        if (mode == 0) break;
+        for (int f = t; f < F; f += RED_NT)
+          if ((mode == 1 && inf[f]) || (mode == 2 && f == ctl[1])) pas[f] ^= 1;
+        __syncthreads();
+      }
+      for (int f = t; f < F; f += RED_NT) sH[j * F + f] = fmax(vx[f], 0.0);
+      __syncthreads();
+    }
+    for (int e = t; e < k * F; e += RED_NT) H64[e] = sH[e];
+    __syncthreads();  // workgroup-scope fence + barrier: the H64 stores are visible to this workgroup
+  }
+  // Ht / HHt of the (new) H, then the passive-set table of the next W-step
+  basis_update_block(nullptr, H64, Ht, HHt, F, k, KP, 0.0, 0.0, 0, nullptr, reinterpret_cast<double*>(smem));
+  __syncthreads();
+  if (t < 16) {
+    const int mask = t;
+    double T[16];
+    for (int e = 0; e < 16; ++e) T[e] = 0.0;
+    bool valid = (mask >> k) == 0 || k >= 4;
+    if (k < 4 && (mask >> k) != 0) valid = false;
+    int P[4], n = 0;
+    for (int j = 0; j < 4; ++j)
+      if (mask >> j & 1) P[n++] = j;
+    if (valid && n > 0) {
+      double a[4][8];
+      double dmax = 0.0;
+      for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+          a[r][c] = HHt[P[r] * KP + P[c]] + delta2;
+          a[r][4 + c] = r == c ? 1.0 : 0.0;
+          if (r == c) dmax = fmax(dmax, fabs(a[r][c]));
+        }
+      for (int c = 0; c < n && valid; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < n; ++r)
+          if (fabs(a[r][c]) > fabs(a[piv][c])) piv = r;
+        if (!(fabs(a[piv][c]) > 1e-13 * dmax)) {
+          valid = false;
+          break;
+        }
+        if (piv != c)
+          for (int e = 0; e < 8; ++e) {
+            const double tmp = a[c][e];
+            a[c][e] = a[piv][e];
+            a[piv][e] = tmp;
+          }
+        const double inv = 1.0 / a[c][c];
+        for (int e = 0; e < 8; ++e) a[c][e] *= inv;
+        for (int r = 0; r < n; ++r) {
+          if (r == c) continue;
+          const double fct = a[r][c];
+          for (int e = 0; e < 8; ++e) a[r][e] -= fct * a[c][e];
+        }
+      }
+      if (valid)
+        for (int r = 0; r < n; ++r)
+          for (int c = 0; c < n; ++c) T[P[r] * 4 + P[c]] = a[r][4 + c];
+    }
+    for (int e = 0; e < 16; ++e) table[mask * 16 + e] = valid ? T[e] : 0.0;
+    table[256 + mask] = valid ? 1.0 : 0.0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Deterministic fp64 reduction of partials[n_parts][n_out]; optional fused basis update.
 // grid = (ceil(n_out/64), nslice): block (c, s) sums rows of slice s for 64 outputs (<= 8 rows per
 // thread, one batch of independent loads) and writes one stage row write-through (sc1); one lane
@@ -1727,6 +2009,23 @@ template <typename TX, int KP, int FT, int NPW, bool SPLIT>
 static PassKernel make_pk() {
   return PassKernel{reinterpret_cast<PassFn>(&mu_pass_kernel<TX, KP, FT, NPW, SPLIT>), KP, NPW, SPLIT,
                     sizeof(TX), sizeof(typename Compute<TX>::T)};
+}
+
+template <typename TX, int FT, int NPW, bool SPLIT>
+static PassKernel make_pk_als() {
+  return PassKernel{reinterpret_cast<PassFn>(&mu_pass_kernel<TX, 4, FT, NPW, SPLIT, true>), 4, NPW, SPLIT,
+                    sizeof(TX), sizeof(typename Compute<TX>::T)};
+}
+
+// the constrained-ALS W-step pass (k <= 4): the VALU pass kernel with the ALS phase 2 and fp64 Ht
+template <typename TX>
+static bool pick_als_tx(int F, int np, PassKernel* out) {
+  if (np <= 1) { *out = make_pk_als<TX, 0, 1, true>(); return true; }
+  if (np == 2) { *out = make_pk_als<TX, 0, 2, true>(); return true; }
+  const int npw = (np + NWAVE - 1) / NWAVE;
+  if (npw <= 2) { *out = make_pk_als<TX, 0, 2, false>(); return true; }
+  if (npw <= 4) { *out = make_pk_als<TX, 0, 4, false>(); return true; }
+  return false;
 }
 
 template <typename TX, int KP>
@@ -2053,6 +2352,76 @@ int cnmf_normalise(void* W, int w_dtype, double* H64, double* Ht, double* HHt, d
     hipLaunchKernelGGL(scale_columns_kernel<double>, dim3(blocks), dim3(256), 0, hs, static_cast<double*>(W),
                        scale, n, k);
   HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_als_table_doubles(void) { return ALS_TAB; }
+
+static int als_basis_launch(const double* AB, double* H64, double* Ht, double* HHt, double* table, int F,
+                            int k, double lam, double delta, int do_update, hipStream_t s) {
+  int st = check_update_args(H64, Ht, HHt, F, k);
+  if (st) return st;
+  if (!table || (do_update && !AB)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (k > 4) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= 4 (got %d)", k);
+  if (F > ALS_MAX_F) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports F <= %d", ALS_MAX_F);
+  if (!(lam >= 0.0) || !(delta >= 0.0)) return set_err(CNMF_ERR_ARG, "smoothness and sum_to_one must be >= 0");
+  const size_t lds = std::max(als_lds_bytes(F, k), update_lds_doubles(F, k, 4) * sizeof(double));
+  if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the ALS update");
+  if (lds > 64 * 1024)
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&als_basis_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(als_basis_kernel, dim3(1), dim3(RED_NT), lds, s, AB, H64, Ht, HHt, table, F, k, 4, lam,
+                     delta * delta, do_update);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_als_prepare(double* H64, double* Ht, double* HHt, double* table, int n_features, int k,
+                     double sum_to_one, void* stream) {
+  return als_basis_launch(nullptr, H64, Ht, HHt, table, n_features, k, 0.0, sum_to_one, 0,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+int cnmf_als_basis_update(const double* AB, double* H64, double* Ht, double* HHt, double* table,
+                          int n_features, int k, double smoothness, double sum_to_one, void* stream) {
+  return als_basis_launch(AB, H64, Ht, HHt, table, n_features, k, smoothness, sum_to_one, 1,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
+int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, const double* table,
+                         double* partials, int64_t n_rows, int n_features, int k, double sum_to_one,
+                         int accumulate, void* stream) {
+  if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
+  if (!X || !W || !Ht || !table || (accumulate && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (k > 4) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= 4 (got %d)", k);
+  if (!(sum_to_one >= 0.0)) return set_err(CNMF_ERR_ARG, "sum_to_one must be >= 0");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+  PassKernel pmain;
+  size_t lmain = 0;
+  int st = select_pass(x_dtype, n_features, k, &pmain, &lmain);
+  if (st) return st;
+  const int64_t nb = main_grid(n_rows, x_dtype, n_features, k, &pmain, &lmain);  // = partial rows
+  if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (nb == 0) return CNMF_OK;
+  PassKernel pk;
+  const int np = (n_features + k + 63) / 64;
+  bool ok = false;
+  switch (x_dtype) {
+    case CNMF_F32: ok = pick_als_tx<float>(n_features, np, &pk); break;
+    case CNMF_F64: ok = pick_als_tx<double>(n_features, np, &pk); break;
+    case CNMF_BF16: ok = pick_als_tx<bf16_t>(n_features, np, &pk); break;
+  }
+  if (!ok) return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d too wide for the ALS pass", n_features);
+  const size_t lds = pass_lds(n_features, 4, pk.sx, pk.sc, 8).total;
+  if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d needs too much LDS", n_features);
+  if (max_resident(pk.fn, lds) <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  int F = n_features;
+  int flags = CNMF_PASS_UPDATE_W | (accumulate ? CNMF_PASS_ACCUMULATE : 0);
+  double d2 = sum_to_one * sum_to_one, zero = 0.0;
+  const int64_t n_tiles = (n_rows + TS - 1) / TS;
+  void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&table, &partials, &n_rows, &F, &k, &d2, &zero, &flags, (void*)&n_tiles};
+  HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, reinterpret_cast<hipStream_t>(stream)));
   return CNMF_OK;
 }
 

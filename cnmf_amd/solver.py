@@ -232,3 +232,60 @@ def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool 
     if return_errors:
         return it, errors
     return it
+
+
+class ALSPlan(MUPlan):
+    """Device state of the constrained-ALS variant (spec and oracle:
+    oracle/als_ref.py, DESIGN.md §Constrained ALS).
+
+    Per iteration: the W-step pass (exact per-sample FCLS, δ = sum_to_one; one HBM pass that also
+    accumulates [WᵀX | WᵀW] of the new W), the deterministic fp64 reduction, (multi-GPU: one
+    all_reduce of the k(F+k) accumulators,) and the H-step (one Gauss-Seidel sweep of exact
+    smoothness-penalised NNLS rows, λ = smoothness) that also rebuilds the W-step's table."""
+
+    def __init__(self, X: torch.Tensor, n_components: int, sum_to_one=0.0, smoothness=0.0, group=None):
+        super().__init__(X, n_components, group=group)
+        if self.k > 4:
+            raise _lib.HipLibraryError(f"constrained ALS supports n_components <= 4 (got {self.k})")
+        self.persistent = False  # the persistent kernel runs the MU update only
+        self.persistent_shape = False
+        self.delta = float(sum_to_one or 0.0)
+        self.lam = float(smoothness or 0.0)
+        if self.delta < 0 or self.lam < 0:
+            raise ValueError("sum_to_one and smoothness must be >= 0")
+        self.table = torch.zeros(int(self.lib.cnmf_als_table_doubles()), dtype=torch.float64,
+                                 device=self.device)
+
+    def refresh_basis(self):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_als_prepare(_ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                                            _ptr(self.table), self.F, self.k, self.delta,
+                                            self._stream()), "cnmf_als_prepare")
+
+    def w_step(self, accumulate: bool = True):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_als_sample_pass(
+                _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.Ht), _ptr(self.table),
+                _ptr(self.partials), self.n_rows, self.F, self.k, self.delta, int(accumulate),
+                self._stream()), "cnmf_als_sample_pass")
+
+    def h_step(self):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_als_basis_update(
+                _ptr(self.AB), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt), _ptr(self.table),
+                self.F, self.k, self.lam, self.delta, self._stream()), "cnmf_als_basis_update")
+
+    def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
+        ev = list(pass_events) if pass_events is not None else None
+        stream = torch.cuda.current_stream(self.device) if ev is not None else None
+        for i in range(max(n_iter, 0)):
+            if ev is not None:
+                ev[2 * i].record(stream)
+            self.w_step(accumulate=update_H)
+            if ev is not None:
+                ev[2 * i + 1].record(stream)
+            if not update_H:
+                continue
+            self.reduce(self.n_out, self.AB)
+            self._allreduce(self.AB)
+            self.h_step()

@@ -137,6 +137,29 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
 int cnmf_normalise(void* W, int w_dtype, double* H64, double* Ht, double* HHt, double* scale,
                    int64_t n_rows, int n_features, int k, int norm, void* stream);
 
+/* ---- Constrained ALS (no sklearn counterpart — the spec and its
+ * scipy-NNLS oracle are oracle/als_ref.py; DESIGN.md §Constrained ALS).  k <= 4, F <= 512.
+ * table: cnmf_als_table_doubles() doubles = the W-step's passive-set inverses of
+ * Q = HHᵀ + δ²11ᵀ (δ = sum_to_one), rebuilt by every basis call. */
+int cnmf_als_table_doubles(void);
+
+/* Ht / HHt / table from H64 (no update): before the first W-step. */
+int cnmf_als_prepare(double* H64, double* Ht, double* HHt, double* table, int n_features, int k,
+                     double sum_to_one, void* stream);
+
+/* The W-step over all samples (one HBM pass): w_i = argmin_{w>=0} ‖x_i − Hᵀw‖² + δ²(1ᵀw − 1)²
+ * exactly (passive-set enumeration on the Gram form), written to W; with accumulate, the
+ * per-workgroup fp64 partials of [WᵀX | WᵀW] of the new W (rows: cnmf_pass_blocks). */
+int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, const double* table,
+                         double* partials, int64_t n_rows, int n_features, int k, double sum_to_one,
+                         int accumulate, void* stream);
+
+/* The H-step on the reduced AB = [WᵀX | WᵀW]: one Gauss-Seidel sweep of exact NNLS rows
+ * h_j = argmin_{h>=0} ½hᵀ(B_jj I + λDᵀD)h − (a_j − Σ_{m≠j} B_jm h_m)ᵀh (λ = smoothness, D the
+ * second difference), then Ht, HHt and the table for the next W-step. */
+int cnmf_als_basis_update(const double* AB, double* H64, double* Ht, double* HHt, double* table,
+                          int n_features, int k, double smoothness, double sum_to_one, void* stream);
+
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);

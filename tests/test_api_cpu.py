@@ -30,6 +30,10 @@ def test_drop_in_name_reexports():
     (dict(init="bogus"), "'init' parameter"),
     (dict(n_components=0), "'n_components' parameter"),
     (dict(normalise="l3"), "'normalise' parameter"),
+    (dict(solver="als", alpha_W=0.1), "no alpha_W"),
+    (dict(solver="als", sum_to_one=-1.0), "'sum_to_one' parameter"),
+    (dict(solver="als", smoothness="x"), "'smoothness' parameter"),
+    (dict(smoothness=1.0), "solver='als' only"),
 ])
 def test_invalid_params(X, kw, msg):
     with pytest.raises(ValueError, match=msg):

@@ -1,0 +1,137 @@
+"""GPU parity of the constrained ALS against oracle/als_ref.py.
+
+The oracle solves every per-sample FCLS and every basis row with scipy's NNLS on identical inputs
+(the fp32 data promoted to fp64); the GPU solves them exactly by other means (passive-set
+enumeration on the Gram form; block principal pivoting with a banded Cholesky), so agreement is
+to fp rounding: W / H within the north_star's 1e-5 relative Frobenius.
+"""
+import numpy as np
+import pytest
+
+from golden_io import rel_fro
+from oracle import als_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(N, F, k, seed):
+    from cnmf_amd.synthetic import iop_spectra
+    X = iop_spectra(N, F, seed=seed, dtype=np.float32)
+    rng = np.random.default_rng(seed)
+    H0 = (rng.random((k, F)) * X.mean() + 1e-3).astype(np.float32)
+    W0 = rng.random((N, k)).astype(np.float32)
+    return X, W0, H0
+
+
+def _plan(X, W0, H0, delta, lam):
+    import torch
+    from cnmf_amd.solver import ALSPlan
+    plan = ALSPlan(torch.from_numpy(X).cuda(), H0.shape[0], sum_to_one=delta, smoothness=lam)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    return plan
+
+
+def _mixtures(N, F, k, seed):
+    """Linear mixtures of k endmember spectra with sparse abundances plus noise: NNLS / FCLS
+    solutions then sit on the bounds for many samples."""
+    from cnmf_amd.synthetic import iop_spectra
+    rng = np.random.default_rng(seed)
+    H = iop_spectra(k, F, seed=seed + 1, dtype=np.float64) + 0.01
+    Wt = rng.dirichlet(0.3 * np.ones(k), size=N)
+    X = np.clip(Wt @ H + 0.01 * H.mean() * rng.standard_normal((N, F)), 0, None).astype(np.float32)
+    H0 = (H * (1 + 0.05 * rng.standard_normal(H.shape))).clip(1e-4).astype(np.float32)
+    return X, rng.random((N, k)).astype(np.float32), H0
+
+
+@pytest.mark.parametrize("F", [81, 300])
+@pytest.mark.parametrize("k", [2, 3, 4])
+@pytest.mark.parametrize("delta", [0.0, 1.0, 5.0])
+def test_w_step_matches_scipy_nnls(F, k, delta):
+    import torch
+    X, W0, H0 = _mixtures(1500 + 37, F, k, seed=F + k)
+    plan = _plan(X, W0, H0, delta, 0.0)
+    plan.w_step(accumulate=True)
+    plan.reduce(plan.n_out, plan.AB)
+    torch.cuda.synchronize()
+    Wg = plan.W.cpu().numpy().astype(np.float64)
+    Wr = als_ref.fcls_w(X.astype(np.float64), H0.astype(np.float64), delta)
+    # c = Hx is formed like the MU numerator (fp32 chains of 7 folded into fp64, ~1e-7 relative);
+    # the solve amplifies that by cond(Q_PP) (near-collinear endmembers here), hence the 1e-5 bar
+    assert rel_fro(Wg, Wr) < 1e-5, rel_fro(Wg, Wr)
+    assert (Wg >= 0).all()
+    if k == 4:
+        assert (Wr == 0).any()  # active bounds are exercised
+    AB = plan.AB.cpu().numpy().reshape(k, F + k)
+    Xd = X.astype(np.float64)
+    np.testing.assert_allclose(AB[:, :F], Wg.T @ Xd, rtol=2e-6)
+    np.testing.assert_allclose(AB[:, F:], Wg.T @ Wg, rtol=2e-6)
+
+
+@pytest.mark.parametrize("F", [17, 81, 300])
+@pytest.mark.parametrize("lam", [0.0, 0.5, 20.0])
+def test_h_step_matches_scipy_nnls(F, lam):
+    import torch
+    k = 4
+    X, W0, H0 = _data(2000, F, k, seed=3 * F)
+    Wr = als_ref.fcls_w(X.astype(np.float64), H0.astype(np.float64), 1.0)
+    A, B = Wr.T @ X.astype(np.float64), Wr.T @ Wr
+    A[1] -= 0.6 * A[1].max()  # force active bounds in the basis rows
+    plan = _plan(X, W0, H0, 1.0, lam)
+    plan.AB.copy_(torch.from_numpy(np.concatenate([A, B], axis=1).ravel()))
+    plan.h_step()
+    torch.cuda.synchronize()
+    Hg = plan.H64.cpu().numpy()
+    Hr = als_ref.smooth_h_sweep(A, B, H0.astype(np.float64), lam)
+    assert rel_fro(Hg, Hr) < 1e-9, rel_fro(Hg, Hr)
+    assert (Hr[1] == 0).any()
+    np.testing.assert_allclose(plan.HHt.cpu().numpy(), Hg @ Hg.T, rtol=1e-12)
+
+
+@pytest.mark.parametrize("delta, lam", [(0.0, 0.0), (1.0, 0.5), (3.0, 5.0)])
+def test_als_fit_matches_oracle(delta, lam):
+    import cnmf_amd
+    X, W0, H0 = _data(3000, 81, 4, seed=11)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom",
+                                 solver="als", sum_to_one=delta, smoothness=lam, tol=0.0,
+                                 max_iter=30)
+    assert n == 30
+    Wr, Hr, _ = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                max_iter=30, tol=0.0, sum_to_one=delta, smoothness=lam)
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_als_tol_stop_matches_oracle():
+    import cnmf_amd
+    X, W0, H0 = _data(2000, 81, 3, seed=12)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=3, init="custom",
+                                 solver="als", sum_to_one=1.0, smoothness=0.1, tol=1e-3,
+                                 max_iter=200)
+    Wr, Hr, nr = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                 max_iter=200, tol=1e-3, sum_to_one=1.0, smoothness=0.1)
+    assert n == nr
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5
+
+
+def test_als_full_size_properties():
+    """cfg5 at full size (1e6 x 81, k=4): finite error, simplex-near abundances, determinism."""
+    import torch
+    from cnmf_amd.solver import ALSPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1_000_000, 81, seed=0, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    Xd = torch.from_numpy(X).cuda()
+    outs = []
+    for rep in range(2):
+        plan = ALSPlan(Xd, 4, sum_to_one=10.0, smoothness=1.0)
+        plan.set_W(torch.from_numpy(W0))
+        plan.set_H(torch.from_numpy(H0))
+        e0 = plan.frobenius_error()
+        plan.iterate(15)
+        e = plan.frobenius_error()
+        assert np.isfinite(e) and e < e0
+        outs.append((plan.W.clone(), plan.H64.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    W = outs[0][0].double()
+    assert bool((W >= 0).all())
+    assert float((W.sum(1) - 1).abs().mean()) < 0.05

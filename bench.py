@@ -42,6 +42,10 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--solver", default="mu", choices=["mu", "als"],
+                   help="mu: cfg2 (the headline); als: cfg5, the constrained ALS")
+    p.add_argument("--sum-to-one", type=float, default=1.0, help="ALS sum-to-one weight (delta)")
+    p.add_argument("--smoothness", type=float, default=0.5, help="ALS smoothness penalty (lambda)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
@@ -80,6 +84,30 @@ def cpu_baseline(X, W0, H0, budget_s):
             "seconds": round(el, 3)}
 
 
+def cpu_baseline_als(X, W0, H0, delta, lam, budget_s):
+    """The ALS oracle (oracle/als_ref.py, scipy NNLS per sample) on a bounded row sample, scaled
+    to iterations/s of the full problem (the per-sample solves dominate and scale linearly)."""
+    from oracle import als_ref
+    n = X.shape[0]
+    rows = 2000
+    Xs = X[:rows].astype(np.float64)
+    H = H0.astype(np.float64)
+    t0 = time.perf_counter()
+    it = 0
+    while True:
+        W = als_ref.fcls_w(Xs, H, delta)
+        H = als_ref.smooth_h_sweep(W.T @ Xs, W.T @ W, H, lam)
+        it += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or it >= 50:
+            break
+    per_it_full = el / it * (n / rows)
+    return {"value": round(1.0 / per_it_full, 6), "unit": "it/s", "cores": 1, "kind": "port",
+            "sample": f"{it} ALS iterations of oracle/als_ref.py (scipy.optimize.nnls per sample, "
+                      f"fp64, 1 thread) on the first {rows} of the {n} rows, scaled by {n}/{rows}",
+            "seconds": round(el, 3)}
+
+
 def load_traffic(path, n_rows, F, k):
     """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py)."""
     try:
@@ -109,7 +137,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.solver import ALSPlan, MUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
 
     n_rows, F, k = args.rows, args.features, args.k
@@ -123,7 +151,10 @@ def main():
     H0d = torch.from_numpy(H0).to(dev)
     if world > 1:
         dist.broadcast(H0d, src=0)
-    plan = MUPlan(Xd, k)
+    if args.solver == "als":
+        plan = ALSPlan(Xd, k, sum_to_one=args.sum_to_one, smoothness=args.smoothness)
+    else:
+        plan = MUPlan(Xd, k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     torch.cuda.synchronize()
@@ -180,10 +211,12 @@ def main():
             dist.destroy_process_group()
         return
 
-    traffic, traffic_src = load_traffic(args.traffic_json, n_rows, F, k)
+    traffic, traffic_src = (None, None) if args.solver == "als" else load_traffic(args.traffic_json, n_rows, F, k)
     if traffic is not None:
         traffic = traffic * iters_per_launch
-    if persistent:
+    if args.solver == "als":
+        kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
+    elif persistent:
         kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
                  "update per launch)")
     elif plan.persistent_shape:
@@ -204,12 +237,25 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu:
         Xc = X if args.dtype != "bf16" else Xt.float().numpy()
-        cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
+        if args.solver == "als":
+            cpu = cpu_baseline_als(Xc, W0, H0, args.sum_to_one, args.smoothness, args.cpu_seconds)
+        else:
+            cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
 
     total_units = world * n_rows / 1e6
     value = total_units * K / elapsed
+    if args.solver == "als":
+        metric = ("constrained-ALS iterations/sec (cfg5: V=1e6x81 k=4, sum-to-one + smoothness) & "
+                  "achieved HBM GB/s of the W-step pass vs peak")
+        workload = (f"cfg5: constrained ALS (FCLS W-step delta={args.sum_to_one}, smoothness "
+                    f"lambda={args.smoothness} NNLS basis sweep, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+                    f"{args.dtype} synthetic IOP spectra")
+    else:
+        metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
+        workload = (f"cfg2: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+                    f"{args.dtype} synthetic IOP spectra; rows sharded across GPUs")
     out = {
-        "metric": "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak",
+        "metric": metric,
         "value": round(value, 2),
         "unit": "it/s",
         "n_gpus": world,
@@ -221,8 +267,7 @@ def main():
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f64": "f64", "bf16": "bf16 X / f32 W"}[args.dtype],
         "data": "synthetic",
-        "config": {"workload": f"cfg2: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
-                               f"{args.dtype} synthetic IOP spectra; rows sharded across GPUs",
+        "config": {"workload": workload,
                    "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
                    "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64)"},
         "roofline": roofline,

@@ -802,6 +802,264 @@ __global__ __launch_bounds__(NT, FT > 0 ? (KP == 16 ? 2 : (KP == 8 ? 3 : 4)) : 2
 }
 
 // ------------------------------------------------------------------------------------------------
+// The bf16 matrix-core pass (X bf16, F = 300, k = 16; any F % 4 == 0,
+// F <= 384, 9 <= k <= 16).  One workgroup = 4 waves, 64-sample tiles, register prefetch one tile
+// ahead (as mu_pass_kernel).  Both per-sample products run on v_mfma_f32_16x16x32_bf16:
+//   phase 1  num[s][n] = Σ_f x[s][f]·H[n][f]   wave = 16 samples (M), N = 16 components, K = F in
+//            steps of 32; A = X rows (ds_read_b64 pairs), B = H rows from LDS (ds_read_b128).
+//   phase 2  lane = (4 samples, component): den = Σ_m w[s][m]·HHt[n][m] (fp64), the MU update
+//            (SK:526-631) in fp64, W' -> HBM and to LDS transposed (W'ᵀ [16][68] fp32).
+//   phase 3  acc[m][f] += Σ_s w'[s][m]·x[s][f]   M = 16 components, K = the tile's 64 samples, N =
+//            the wave's 16-feature blocks (nb ≡ wave mod 4); B = X columns via ds_read_b64_tr_b16
+//            (the hardware transpose read, one image for row and column reads); and
+//            B[m][n] += Σ_s w'[s][m]·w'[s][n] on v_mfma_f32_16x16x4_f32 (the wave's 16 samples).
+// Precision: X is exact in bf16; H and W' are each split into three bf16 terms (h = h1+h2+h3 to
+// ~2^-27 relative) so every product X·h_i is exact in fp32, and each tile's fp32 MFMA sums are
+// folded into fp64 accumulators (the 1e-5 bar of DESIGN.md §Precision).
+// ------------------------------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+namespace bm {
+constexpr int KP = 16;
+constexpr int PFN = 11;      // 16-byte chunks per thread prefetched (tiles up to 44 KB: F <= 320)
+constexpr int NBW_MAX = 5;   // 16-feature blocks per wave in phase 3 (F <= 320)
+constexpr int WNT_ROW = 68;  // W'ᵀ row stride in floats (conflict-free transposed writes)
+struct Lds {
+  int x, w, wnt, hs, hht, total, hrow;  // byte offsets; hrow = bytes per H-split row
+};
+__host__ __device__ inline int ksteps(int F) { return (F + 31) / 32; }
+__host__ __device__ inline Lds lds(int F) {
+  Lds L;
+  L.x = 0;
+  L.w = (int)align16((size_t)TS * F * 2 + 64);        // + 64 zero bytes for the padded reads
+  L.wnt = L.w + TS * KP * 4;
+  L.hs = L.wnt + KP * WNT_ROW * 4;
+  L.hrow = (32 * ksteps(F) + 8) * 2;                   // +16 B: conflict-free b128 row reads
+  L.hht = L.hs + 3 * KP * L.hrow;
+  L.total = L.hht + KP * KP * 8;
+  return L;
+}
+__device__ __forceinline__ uint16_t bf16_rn(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf16_f(uint16_t b) { return __uint_as_float((uint32_t)b << 16); }
+}  // namespace bm
+
+__global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* __restrict__ X,
+                                                                 float* __restrict__ W,
+                                                                 const double* __restrict__ Ht,
+                                                                 const double* __restrict__ HHt,
+                                                                 double* __restrict__ partials,
+                                                                 int64_t n_rows, int F, int k, double l1,
+                                                                 double l2, int flags, int64_t n_tiles) {
+  using namespace bm;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Lds L = lds(F);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = lane >> 4;   // 16-lane group
+  const int li = lane & 15;  // index inside the group
+  const int KS = ksteps(F);
+  const int NB = (F + 15) / 16;
+  const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+  float* sWnT = reinterpret_cast<float*>(smem + L.wnt);
+  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
+
+  // ---- basis constants: H split into three bf16 rows [n][32·KS] (zero beyond F / k), HHt
+  for (int e = t; e < KP * 32 * KS; e += NT) {
+    const int n = e / (32 * KS);
+    const int f = e - n * 32 * KS;
+    const double h = (n < k && f < F) ? Ht[(size_t)f * KP + n] : 0.0;
+    const uint16_t h1 = bf16_rn((float)h);
+    const double r1 = h - (double)bf16_f(h1);
+    const uint16_t h2 = bf16_rn((float)r1);
+    const double r2 = r1 - (double)bf16_f(h2);
+    const uint16_t h3 = bf16_rn((float)r2);
+    uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;  // split i at +i·KP rows
+    row[0] = h1;
+    row[KP * L.hrow / 2] = h2;
+    row[2 * KP * L.hrow / 2] = h3;
+  }
+  for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
+  for (int e = t; e < 16; e += NT) reinterpret_cast<uint32_t*>(smem + L.x + TS * F * 2)[e] = 0u;
+  __syncthreads();
+
+  // phase 3 accumulators (A part: the wave's feature blocks; B part) in fp64, per-tile fp32 MFMA sums
+  double acc64[NBW_MAX][4];
+  double bacc64[4];
+#pragma unroll
+  for (int i = 0; i < NBW_MAX; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[i][r] = 0.0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bacc64[r] = 0.0;
+
+  u32x4 pf[PFN];
+  int64_t tile = blockIdx.x;
+  if (tile < n_tiles) prefetch_tile<PFN>(pf, tile_geom(X, W, tile, n_rows, F, k), t);
+
+  for (; tile < n_tiles; tile += gridDim.x) {
+    const TileGeom gm = tile_geom(X, W, tile, n_rows, F, k);
+    const int ns = gm.ns;
+    stage_tile<bf16_t, float, PFN>(smem, L.w, gm, pf, t, F);
+    if (ns < TS) {  // ragged tile: rows >= ns must hold finite values for the MFMA reads
+      uint16_t* sx = reinterpret_cast<uint16_t*>(smem + L.x);
+      for (int e = ns * F + 4 + t; e < TS * F; e += NT) sx[e] = 0;
+    }
+    __syncthreads();
+    {
+      const int64_t nt = tile + gridDim.x;
+      if (nt < n_tiles) prefetch_tile<PFN>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
+    }
+
+    // ---- phase 1: num for samples 16·wave + (4g + r), component li
+    f32x4 num;
+    double num64[4] = {0.0, 0.0, 0.0, 0.0};
+    {
+      const unsigned char* xa = smem + L.x + ((size_t)(16 * wave + li) * F + 8 * g) * 2;
+      const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
+      for (int ks = 0; ks < KS; ++ks) {
+        const uint64_t a0 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks);
+        const uint64_t a1 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks + 8);
+        s16x8 a;
+        a.s0123 = __builtin_bit_cast(s16x4, a0);
+        a.s4567 = __builtin_bit_cast(s16x4, a1);
+        const s16x8 b1 = *reinterpret_cast<const s16x8*>(hb + 64 * ks);
+        const s16x8 b2 = *reinterpret_cast<const s16x8*>(hb + KP * L.hrow + 64 * ks);
+        const s16x8 b3 = *reinterpret_cast<const s16x8*>(hb + 2 * KP * L.hrow + 64 * ks);
+        const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+        num = f32x4{0.f, 0.f, 0.f, 0.f};
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b3), num, 0, 0, 0);
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b2), num, 0, 0, 0);
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b1), num, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) num64[r] += (double)num[r];
+      }
+    }
+
+    // ---- phase 2: MU update of w[s][n], s = 16·wave + 4g + r, n = li (SK:526-631)
+    if (do_upd) {
+      const float* sWo = reinterpret_cast<const float*>(smem + L.w);
+      const double* hh = sHHt + li * KP;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = 16 * wave + 4 * g + r;
+        float wn = 0.f;
+        if (s < ns && li < k) {
+          double den = 0.0;
+          for (int m = 0; m < k; ++m) den = fma((double)sWo[s * k + m], hh[m], den);
+          const double wold = (double)sWo[s * k + li];
+          if (l1 > 0.0) den += l1;              // SK:616-617
+          if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
+          if (den == 0.0) den = EPS32;          // SK:620
+          wn = (float)(wold * (num64[r] / den));  // SK:622-629
+          W[(size_t)(tile * TS + s) * k + li] = wn;
+        }
+        sWnT[li * WNT_ROW + s] = wn;
+      }
+    }
+    __syncthreads();  // every wave's W'ᵀ rows feed every wave's phase 3
+
+    // ---- phase 3: acc[m = 4g + r][f = 16·nb + li] += Σ_s w'[s][m]·x[s][f]; B on f32 MFMA
+    if (do_acc) {
+      f32x4 cacc[NBW_MAX];
+#pragma unroll
+      for (int i = 0; i < NBW_MAX; ++i) cacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int ks2 = 0; ks2 < 2; ++ks2) {
+        // A operand: W'ᵀ[m = li][s = 32·ks2 + 8g + j], split into three bf16 terms
+        const float* wr = sWnT + li * WNT_ROW + 32 * ks2 + 8 * g;
+        const float4 w0 = *reinterpret_cast<const float4*>(wr);
+        const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
+        const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        s16x8 a1, a2, a3;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint16_t h1 = bf16_rn(wv[j]);
+          const float r1 = wv[j] - bf16_f(h1);
+          const uint16_t h2 = bf16_rn(r1);
+          const float r2 = r1 - bf16_f(h2);
+          a1[j] = (short)h1;
+          a2[j] = (short)h2;
+          a3[j] = (short)bf16_rn(r2);
+        }
+        // B operand: X[s = 32·ks2 + 8g + j][f = 16·nb + li] by two transposed reads (4 rows each)
+        const int q = li >> 2, p = li & 3;
+        const unsigned char* xb0 = smem + L.x + ((size_t)(32 * ks2 + 8 * g + q) * F + 4 * p) * 2;
+#pragma unroll
+        for (int i = 0; i < NBW_MAX; ++i) {
+          const int nb = wave + 4 * i;
+          if (nb < NB) {
+            const unsigned char* xb = xb0 + 32 * nb;
+            const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb));
+            const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb + (size_t)4 * F * 2));
+            s16x8 b;
+            b.s0123 = lo;
+            b.s4567 = hi;
+            const bf16x8 bv = __builtin_bit_cast(bf16x8, b);
+            cacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a3), bv, cacc[i], 0, 0, 0);
+            cacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a2), bv, cacc[i], 0, 0, 0);
+            cacc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1), bv, cacc[i], 0, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NBW_MAX; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc64[i][r] += (double)cacc[i][r];
+      // B part: the wave's 16 samples, K = 4 per f32 MFMA (A = B operand value: W'ᵀ[li][s])
+      f32x4 bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float v = sWnT[li * WNT_ROW + 16 * wave + 4 * kk + g];
+        bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, bacc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bacc64[r] += (double)bacc[r];
+    }
+    __syncthreads();  // LDS tiles are rewritten by the next iteration
+  }
+
+  // ---- per-workgroup partial row [k][F + k]: A from each wave's own blocks, B summed over waves
+  if (do_acc) {
+    const int V = F + k;
+    double* prow = partials + (size_t)blockIdx.x * k * V;
+#pragma unroll
+    for (int i = 0; i < NBW_MAX; ++i) {
+      const int nb = wave + 4 * i;
+      const int f = 16 * nb + li;
+      if (nb < NB && f < F) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 4 * g + r;
+          if (m < k) prow[(size_t)m * V + f] = acc64[i][r];
+        }
+      }
+    }
+    double* red = reinterpret_cast<double*>(smem + L.x);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[(wave * 64 + lane) * 4 + r] = bacc64[r];
+    __syncthreads();
+    {
+      const int l = t & 63, r = t >> 6;  // output B[m = 4(l>>4) + r][n = l & 15]
+      const int m = 4 * (l >> 4) + r, n = l & 15;
+      if (m < k && n < k) {
+        const double sum = ((red[(0 * 64 + l) * 4 + r] + red[(1 * 64 + l) * 4 + r]) +
+                            red[(2 * 64 + l) * 4 + r]) + red[(3 * 64 + l) * 4 + r];
+        prow[(size_t)m * V + F + n] = sum;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // The sample-lane pass: the IOP grid's headline shape (F = 81, k = 4, fp32 X and W), full tiles.
 //
 // mu_pass_kernel spends most of its issue slots and LDS cycles on moving data between lane
@@ -2087,9 +2345,21 @@ static bool use_sl(int x_dtype, int F, int k) {
   return !g_no_sl && x_dtype == CNMF_F32 && F == sl::F && k == sl::K;
 }
 
+// the bf16 matrix-core pass (§8 a8): bf16 X, 9 <= k <= 16, F % 4 == 0 (8-byte aligned rows for the
+// transposed LDS reads), F <= 64·NBW_MAX
+static bool use_bf16_mfma(int x_dtype, int F, int k) {
+  return x_dtype == CNMF_BF16 && k >= 9 && k <= 16 && F % 4 == 0 && F <= 64 * bm::NBW_MAX &&
+         bm::lds(F).total <= (int)(160 * 1024);
+}
+
 static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds, bool mfma_ok = true) {
   if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
   if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
+  if (mfma_ok && !g_force_valu && use_bf16_mfma(x_dtype, F, k)) {
+    *pk = PassKernel{reinterpret_cast<PassFn>(&mu_pass_bf16_mfma_kernel), 16, 0, true, 2, 4};
+    *lds = (size_t)bm::lds(F).total;
+    return CNMF_OK;
+  }
   const int KP = padded_k(k);
   const int np = (F + k + 63) / 64;
   bool ok = mfma_ok && !g_force_valu && pick_mfma(x_dtype, F, k, pk);

@@ -213,3 +213,31 @@ def test_factorise_normalise_option():
     Wn, Hn, _ = mu_ref.normalise(Wr, Hr, "l2")
     assert rel_fro(W, Wn) <= TOL32 and rel_fro(H, Hn) <= TOL32
     np.testing.assert_allclose(np.linalg.norm(H.astype(np.float64), axis=1), 1.0, rtol=1e-6)
+
+
+@pytest.mark.parametrize("N, F, k", [(4096 + 29, 300, 16), (1000, 64, 12), (777, 300, 9), (3000, 124, 16)])
+def test_bf16_mfma_single_pass_matches_numpy(N, F, k):
+    """§8 a8: the bf16 matrix-core pass (v_mfma_f32_16x16x32_bf16 with 3-term bf16 splits of H and
+    W', ds_read_b64_tr_b16 column reads): one W update and [WᵀX | WᵀW] vs NumPy fp64 on the
+    bf16-rounded X (ragged last tile, k < 16 padding)."""
+    import torch
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd import _lib
+    rng = np.random.default_rng(N + F + k)
+    Xb = torch.from_numpy(rng.random((N, F)).astype(np.float32)).to(torch.bfloat16)
+    Xr = Xb.float().numpy().astype(np.float64)
+    W0 = rng.random((N, k)).astype(np.float32)
+    H0 = rng.random((k, F)).astype(np.float32)
+    plan = MUPlan(Xb.cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+    plan.reduce(plan.n_out, plan.AB)
+    torch.cuda.synchronize()
+    Wref, _, _ = mu_ref.update_w(Xr, W0.astype(np.float64), H0.astype(np.float64))
+    Wg = plan.W.cpu().numpy()
+    assert rel_fro(Wg, Wref) < 1e-6, rel_fro(Wg, Wref)
+    AB = plan.AB.cpu().numpy().reshape(k, F + k)
+    Wn = Wg.astype(np.float64)
+    np.testing.assert_allclose(AB[:, :F], Wn.T @ Xr, rtol=2e-6)
+    np.testing.assert_allclose(AB[:, F:], Wn.T @ Wn, rtol=2e-6)

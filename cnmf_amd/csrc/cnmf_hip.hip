@@ -821,6 +821,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
 namespace bm {
 constexpr int KP = 16;
@@ -890,6 +891,9 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
   for (int e = t; e < KP * KP; e += NT) sHHt[e] = HHt[e];
   for (int e = t; e < 16; e += NT) reinterpret_cast<uint32_t*>(smem + L.x + TS * F * 2)[e] = 0u;
   __syncthreads();
+  double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li] (HHᵀ symmetric)
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * KP + li];
 
   // phase 3 accumulators (A part: the wave's feature blocks; B part) in fp64, per-tile fp32 MFMA sums
   double acc64[NBW_MAX][4];
@@ -944,22 +948,31 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
       }
     }
 
-    // ---- phase 2: MU update of w[s][n], s = 16·wave + 4g + r, n = li (SK:526-631)
+    // ---- phase 2: MU update of w[s][n], s = 16·wave + 4g + r, n = li (SK:526-631).
+    // den = W·HHᵀ on v_mfma_f64_16x16x4_f64 (exact fp64 products and sums; f64 C/D layout: row =
+    // g + 4·reg): its A-operand row ρ carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is sample 4g + r,
+    // the lane mapping of num.  HHᵀ (the B operand) lives in 4 registers per lane (hhb).
     if (do_upd) {
       const float* sWo = reinterpret_cast<const float*>(smem + L.w);
-      const double* hh = sHHt + li * KP;
+      f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
+      const int sa = 16 * wave + 4 * (li & 3) + (li >> 2);  // A-operand row li's sample
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int m = 4 * kk + g;
+        const double a = m < k ? (double)sWo[sa * k + m] : 0.0;
+        den = __builtin_amdgcn_mfma_f64_16x16x4f64(a, hhb[kk], den, 0, 0, 0);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int s = 16 * wave + 4 * g + r;
         float wn = 0.f;
         if (s < ns && li < k) {
-          double den = 0.0;
-          for (int m = 0; m < k; ++m) den = fma((double)sWo[s * k + m], hh[m], den);
+          double d = den[r];
           const double wold = (double)sWo[s * k + li];
-          if (l1 > 0.0) den += l1;              // SK:616-617
-          if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
-          if (den == 0.0) den = EPS32;          // SK:620
-          wn = (float)(wold * (num64[r] / den));  // SK:622-629
+          if (l1 > 0.0) d += l1;              // SK:616-617
+          if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
+          if (d == 0.0) d = EPS32;            // SK:620
+          wn = (float)(wold * (num64[r] / d));  // SK:622-629
           W[(size_t)(tile * TS + s) * k + li] = wn;
         }
         sWnT[li * WNT_ROW + s] = wn;
@@ -1423,7 +1436,9 @@ __global__ __launch_bounds__(NT, 3) void mu_pass_sl_kernel(const float* __restri
 // ------------------------------------------------------------------------------------------------
 // Basis update (one workgroup): the k×F epilogue, all in fp64.
 // ------------------------------------------------------------------------------------------------
+__host__ __device__ inline size_t update_mfma_lds_doubles(int F);
 __host__ __device__ inline size_t update_lds_doubles(int F, int k, int KP) {
+  if (KP >= 8) return update_mfma_lds_doubles(F);
   return 2 * (size_t)k * F + (size_t)k * k + (size_t)KP * KP + 2 * (RED_NT / 64);
 }
 
@@ -1433,7 +1448,127 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// The basis update for KP >= 8 on v_mfma_f64_16x16x4_f64 (exact fp64; C/D layout row = g + 4·reg,
+// col = lane & 15; A/B as the f32 16x16x4 form): den = (WᵀW)·H per 16-feature block and HHᵀ = H·Hᵀ
+// with the 4 waves splitting K = F, their partials summed in fixed order.  H is staged in LDS
+// ([16][F16], zero rows >= k and columns >= F) and updated in place; AB is read with sc1 loads.
+// Per element the same arithmetic as basis_update_block (den a k-ordered fma chain, SK:634-728).
+__host__ __device__ inline int f16pad(int F) { return (F + 15) / 16 * 16; }
+__host__ __device__ inline size_t update_mfma_lds_doubles(int F) {
+  return 16 * (size_t)f16pad(F) + 16 * 16 + 4 * 64 * 4 + 2 * 4;
+}
+
+__device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, double* HHt, int F, int k,
+                                  int KP, double l1, double l2, int do_update, double* stats, double* lds) {
+  typedef double f64x4v __attribute__((ext_vector_type(4)));
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int V = F + k;
+  const int FP = f16pad(F);
+  const int NB = FP / 16;
+  double* sH = lds;                   // [16][FP]
+  double* sB = sH + 16 * FP;          // [16][16], zero beyond k
+  double* red = sB + 256;             // [4 waves][64 lanes][4]
+  double* sR = red + 4 * 64 * 4;      // [2][4]
+  const bool upd = do_update && AB != nullptr;
+  for (int e = t; e < 16 * FP; e += RED_NT) {
+    const int j = e / FP, f = e - j * FP;
+    sH[e] = (j < k && f < F) ? H64[j * F + f] : 0.0;
+  }
+  for (int e = t; e < 256; e += RED_NT) {
+    const int j = e >> 4, m = e & 15;
+    sB[e] = (upd && j < k && m < k) ? __hip_atomic_load(AB + j * V + F + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+  }
+  __syncthreads();
+  if (upd) {
+    constexpr int NBL = 8;  // F <= 512
+    double hn[NBL][4];
+    double bfr[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) bfr[kk] = sB[li * 16 + 4 * kk + g];  // A[j = li][m = 4kk + g]
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      const int nb = wave + 4 * i;
+      if (nb >= NB) break;
+      const int f = 16 * nb + li;
+      f64x4v den = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        den = __builtin_amdgcn_mfma_f64_16x16x4f64(bfr[kk], sH[(4 * kk + g) * FP + f], den, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = g + 4 * r;
+        double h = sH[j * FP + f];
+        if (j < k && f < F) {
+          const double num = __hip_atomic_load(AB + j * V + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          double d = den[r];
+          if (l1 > 0.0) d += l1;                                // SK:702-703
+          if (l2 > 0.0) d = d + l2 * h;                         // SK:704-705
+          if (d == 0.0) d = EPS32;                              // SK:706
+          h = h * (num / d);                                    // SK:722-726
+        }
+        hn[i][r] = h;
+      }
+    }
+    __syncthreads();  // every old H read is done before sH is overwritten
+#pragma unroll
+    for (int i = 0; i < NBL; ++i) {
+      const int nb = wave + 4 * i;
+      if (nb >= NB) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sH[(g + 4 * r) * FP + 16 * nb + li] = hn[i][r];
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < k * F; e += RED_NT) H64[e] = sH[(e / F) * FP + (e % F)];
+  for (int e = t; e < F * KP; e += RED_NT) {
+    const int f = e / KP, j = e - f * KP;
+    Ht[e] = j < k ? sH[j * FP + f] : 0.0;
+  }
+  // HHᵀ: K = F in steps of 4 features, step kk on wave kk % 4; A[j = li][f] = B[f][m = li] = H[li][f]
+  f64x4v hh = f64x4v{0.0, 0.0, 0.0, 0.0};
+  for (int kk = wave; 4 * kk < FP; kk += 4) {
+    const double v = sH[li * FP + 4 * kk + g];
+    hh = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, hh, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[(wave * 64 + lane) * 4 + r] = hh[r];
+  __syncthreads();
+  {
+    const int l = t & 63, r = t >> 6;  // entry (j = (l >> 4) + 4r, m = l & 15)
+    const int j = (l >> 4) + 4 * r, m = l & 15;
+    const double v = ((red[(0 * 64 + l) * 4 + r] + red[(1 * 64 + l) * 4 + r]) + red[(2 * 64 + l) * 4 + r]) +
+                     red[(3 * 64 + l) * 4 + r];
+    if (j < KP && m < KP) HHt[j * KP + m] = v;
+    if (stats && upd) {
+      double a = 0.0, b = 0.0;
+      for (int e = t; e < k * F; e += RED_NT)
+        a = fma(__hip_atomic_load(AB + (e / F) * V + (e % F), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                sH[(e / F) * FP + (e % F)], a);
+      if (j < k && m < k) b = sB[j * 16 + m] * v;
+      a = wave_sum(a);
+      b = wave_sum(b);
+      if (lane == 0) {
+        sR[wave] = a;
+        sR[4 + wave] = b;
+      }
+      __syncthreads();
+      if (t == 0) {
+        stats[0] = ((sR[0] + sR[1]) + sR[2]) + sR[3];
+        stats[1] = ((sR[4] + sR[5]) + sR[6]) + sR[7];
+      }
+    }
+  }
+}
+
 __device__ void basis_update_block(const double* AB, double* H64, double* Ht, double* HHt, int F,
+                                   int k, int KP, double l1, double l2, int do_update, double* stats,
+                                   double* lds);
+
+// the KP = 4 basis update (one wave per HHᵀ entry; the arithmetic sl_update_basis repeats)
+__device__ void basis_update_small(const double* AB, double* H64, double* Ht, double* HHt, int F,
                                    int k, int KP, double l1, double l2, int do_update, double* stats,
                                    double* lds) {
   const int t = threadIdx.x;
@@ -1475,17 +1610,20 @@ __device__ void basis_update_block(const double* AB, double* H64, double* Ht, do
     Ht[e] = j < k ? sH[j * F + f] : 0.0;
   }
   // HHt[j][m] = Σ_f H[j][f]·H[m][f]: one wave per entry, lanes over f, fixed-order shuffle tree
-  for (int e = wave; e < KP * KP; e += NWV) {
-    const int j = e / KP;
-    const int m = e - j * KP;
-    double v = 0.0;
-    if (j < k && m < k) {
-      for (int f = lane; f < F; f += 64) v = fma(sH[j * F + f], sH[m * F + f], v);
-      v = wave_sum(v);
-    }
-    if (lane == 0) {
-      sHH[e] = v;
-      HHt[e] = v;
+  // (the arithmetic sl_derive_basis repeats; KP >= 8 takes basis_update_mfma)
+  {
+    for (int e = wave; e < KP * KP; e += NWV) {
+      const int j = e / KP;
+      const int m = e - j * KP;
+      double v = 0.0;
+      if (j < k && m < k) {
+        for (int f = lane; f < F; f += 64) v = fma(sH[j * F + f], sH[m * F + f], v);
+        v = wave_sum(v);
+      }
+      if (lane == 0) {
+        sHH[e] = v;
+        HHt[e] = v;
+      }
     }
   }
   if (stats && have_ab) {
@@ -1510,6 +1648,15 @@ __device__ void basis_update_block(const double* AB, double* H64, double* Ht, do
       stats[1] = sb;
     }
   }
+}
+
+__device__ void basis_update_block(const double* AB, double* H64, double* Ht, double* HHt, int F,
+                                   int k, int KP, double l1, double l2, int do_update, double* stats,
+                                   double* lds) {
+  if (KP >= 8)
+    basis_update_mfma(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats, lds);
+  else
+    basis_update_small(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats, lds);
 }
 
 __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __restrict__ AB,
@@ -1563,7 +1710,9 @@ constexpr int CNT_GROUP0 = 32;
 constexpr int CNT_TOP = CNT_GROUP0 + 32 * sl::MAX_GROUPS;
 constexpr int CNT_FLAG = CNT_TOP + 32;
 constexpr int CNT_ERR = CNT_FLAG + 32;
-constexpr int CNT_WORDS = CNT_ERR + 32;
+constexpr int CNT_RCOL0 = CNT_ERR + 32;          // reduce_kernel: one ticket per 64-column block
+constexpr int RED_MAX_COLS = 512;
+constexpr int CNT_WORDS = CNT_RCOL0 + RED_MAX_COLS;
 
 // sHt (fp32 [84][4], rows >= 81 zero) and sHHt (fp64 [4][4]) from the fp64 H in LDS; the HHᵀ
 // arithmetic (lanes over f, fixed shuffle tree) is that of basis_update_block.
@@ -1939,7 +2088,7 @@ constexpr int ALS_MAX_F = 512;
 
 __host__ __device__ inline size_t als_lds_bytes(int F, int k) {
   // doubles: A, H [k][F]; B [k][k]; b, x, d0, e1, e2, L0, L1, L2, z [F]; then ints: pas, inf, idx [F], 8
-  return ((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 8) * 4;
+  return ((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 16) * 4;
 }
 
 // M(fa, fb) of the row Hessian for |fa - fb| <= 2 (0 otherwise), fb < fa
@@ -2190,35 +2339,59 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
                        __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
+  // the last slice of this 64-column block to arrive combines the block's slices (fixed order:
+  // part r sums slices r, r+4, ...; the 4 parts in order)
+  uint32_t* ccol = counter + CNT_RCOL0 + blockIdx.x;
   if (t == 0) {
-    const uint32_t total = gridDim.x * gridDim.y;
-    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    flag[0] = old == total - 1;
+    const uint32_t old = __hip_atomic_fetch_add(ccol, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = old == (uint32_t)nslice - 1;
   }
   __syncthreads();
   if (!flag[0]) return;
-  double* ab = fuse ? upd : nullptr;
-  for (int oo = t; oo < n_out; oo += RED_NT) {
+  {
     double v = 0.0;
-    for (int s0 = 0; s0 < nslice; s0 += 16) {
+    if (o < n_out) {
       double x[16];
+      for (int s0 = r; s0 < nslice; s0 += 64) {
 #pragma unroll
-      for (int u = 0; u < 16; ++u)
-        x[u] = s0 + u < nslice ? __hip_atomic_load(stage + (size_t)(s0 + u) * n_out + oo, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : 0.0;
+        for (int u = 0; u < 16; ++u) {
+          const int sl = s0 + 4 * u;
+          x[u] = __hip_atomic_load(stage + (size_t)min(sl, nslice - 1) * n_out + o, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v += x[u];
+        for (int u = 0; u < 16; ++u) v += s0 + 4 * u < nslice ? x[u] : 0.0;
+      }
     }
-    out[oo] = v;
-    if (fuse) ab[oo] = v;
+    red[t] = v;
+    __syncthreads();
+    if (r == 0 && o < n_out) {
+      const double sum = ((red[l] + red[64 + l]) + red[128 + l]) + red[192 + l];
+      if (fuse)
+        __hip_atomic_store(out + o, sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        out[o] = sum;
+    }
+    if (t == 0) __hip_atomic_store(ccol, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (t == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (!fuse) return;
+  // every column block done -> the last one applies the basis update
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[1] = old == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!flag[1]) return;
+  if (t == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double* ab = upd;
+  for (int oo = t; oo < n_out; oo += RED_NT)
+    ab[oo] = __hip_atomic_load(out + oo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   double* scratch = upd + ((n_out + 1) & ~1);
-  basis_update_block(ab, ua.H64, ua.Ht, ua.HHt, ua.F, ua.k, ua.KP, ua.l1, ua.l2, 1, ua.stats,
-                     scratch);
+  basis_update_small(ab, ua.H64, ua.Ht, ua.HHt, ua.F, ua.k, ua.KP, ua.l1, ua.l2, 1, ua.stats,
+                     scratch);  // fused only for KP = 4 (cnmf_reduce_update)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2553,6 +2726,7 @@ static int launch_reduce(const double* partials, int64_t n_parts, int n_out, dou
   const int nslice = (int)std::max<int64_t>(1, std::min<int64_t>(NSLICE, (n_parts + 4 * RED_ROWS_PER_THREAD - 1) / (4 * RED_ROWS_PER_THREAD)));
   if ((int64_t)nslice * 4 * RED_ROWS_PER_THREAD < n_parts)
     return set_err(CNMF_ERR_UNSUPPORTED, "too many partial rows (%lld) for one reduction", (long long)n_parts);
+  if ((n_out + 63) / 64 > RED_MAX_COLS) return set_err(CNMF_ERR_UNSUPPORTED, "n_out=%d too wide for the reduction", n_out);
   dim3 grid((unsigned)((n_out + 63) / 64), (unsigned)nslice);
   hipLaunchKernelGGL(reduce_kernel, grid, dim3(RED_NT), lds, s, partials, n_parts, n_out, nslice,
                      stage, counter, out, fuse, ua);
@@ -2573,6 +2747,7 @@ static int check_update_args(const double* H64, const double* Ht, const double* 
   if (!H64 || !Ht || !HHt) return set_err(CNMF_ERR_ARG, "null pointer argument");
   if (F < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", F, k);
   if (k > 16) return set_err(CNMF_ERR_UNSUPPORTED, "k=%d > 16 is not supported", k);
+  if (k > 4 && F > 512) return set_err(CNMF_ERR_UNSUPPORTED, "n_features=%d > 512 with k=%d > 4", F, k);
   return CNMF_OK;
 }
 
@@ -2701,6 +2876,14 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
   int st = check_update_args(H64, Ht, HHt, n_features, k);
   if (st) return st;
   UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats};
+  if (ua.KP >= 8) {
+    // k > 4: the reduction alone (small registers, full occupancy), then the matrix-core basis
+    // update as its own single-workgroup launch (its LDS stages the whole H)
+    st = launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 0, ua,
+                       reinterpret_cast<hipStream_t>(stream));
+    if (st) return st;
+    return cnmf_basis_update(AB, H64, Ht, HHt, n_features, k, l1_H, l2_H, 1, stats, stream);
+  }
   return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,
                        reinterpret_cast<hipStream_t>(stream));
 }

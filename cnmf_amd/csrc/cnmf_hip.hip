@@ -1451,7 +1451,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 // The basis update for KP >= 8 on v_mfma_f64_16x16x4_f64 (exact fp64; C/D layout row = g + 4·reg,
 // col = lane & 15; A/B as the f32 16x16x4 form): den = (WᵀW)·H per 16-feature block and HHᵀ = H·Hᵀ
 // with the 4 waves splitting K = F, their partials summed in fixed order.  H is staged in LDS
-// ([16][F16], zero rows >= k and columns >= F) and updated in place; AB is read with sc1 loads.
+// ([16][F16], zero rows >= k and columns >= F) and updated in place; AB comes from a previous
+// launch (the reduction), so plain loads see it.
 // Per element the same arithmetic as basis_update_block (den a k-ordered fma chain, SK:634-728).
 __host__ __device__ inline int f16pad(int F) { return (F + 15) / 16 * 16; }
 __host__ __device__ inline size_t update_mfma_lds_doubles(int F) {
@@ -1479,7 +1480,7 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
   }
   for (int e = t; e < 256; e += RED_NT) {
     const int j = e >> 4, m = e & 15;
-    sB[e] = (upd && j < k && m < k) ? __hip_atomic_load(AB + j * V + F + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    sB[e] = (upd && j < k && m < k) ? AB[j * V + F + m] : 0.0;
   }
   __syncthreads();
   if (upd) {
@@ -1502,7 +1503,7 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
         const int j = g + 4 * r;
         double h = sH[j * FP + f];
         if (j < k && f < F) {
-          const double num = __hip_atomic_load(AB + j * V + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const double num = AB[j * V + f];
           double d = den[r];
           if (l1 > 0.0) d += l1;                                // SK:702-703
           if (l2 > 0.0) d = d + l2 * h;                         // SK:704-705
@@ -1545,8 +1546,7 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
     if (stats && upd) {
       double a = 0.0, b = 0.0;
       for (int e = t; e < k * F; e += RED_NT)
-        a = fma(__hip_atomic_load(AB + (e / F) * V + (e % F), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                sH[(e / F) * FP + (e % F)], a);
+        a = fma(AB[(e / F) * V + (e % F)], sH[(e / F) * FP + (e % F)], a);
       if (j < k && m < k) b = sB[j * 16 + m] * v;
       a = wave_sum(a);
       b = wave_sum(b);
@@ -2156,39 +2156,73 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
       }
       __syncthreads();
       int alpha = 3, beta = F + 1;  // BPP control (thread 0's copy is the one that counts)
+      const int lane = t & 63, wave = t >> 6;
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
+        // ---- compress the passive set in parallel (ballot prefix per wave, waves in order;
+        // per-wave counts in ctl[4 + 4c + wave])
+        int pos[2];
+        bool pp[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int f = c * RED_NT + t;
+          pp[c] = f < F && pas[f];
+          const uint64_t bal = __ballot(pp[c]);
+          pos[c] = __popcll(bal & ((1ull << lane) - 1ull));
+          if (lane == 0) ctl[4 + c * 4 + wave] = __popcll(bal);
+        }
+        for (int f = t; f < F; f += RED_NT) vx[f] = 0.0;
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          int base = 0;
+          for (int u = 0; u < c * 4 + wave; ++u) base += ctl[4 + u];
+          if (pp[c]) idx[base + pos[c]] = c * RED_NT + t;
+        }
         if (t == 0) {
-          // compress the passive set, banded Cholesky of M_PP, forward / backward substitution
-          int n = 0;
-          for (int f = 0; f < F; ++f) {
-            vx[f] = 0.0;
-            if (pas[f]) idx[n++] = f;
-          }
+          int nn = 0;
+          for (int u = 0; u < 8; ++u) nn += ctl[4 + u];
+          ctl[3] = nn;
+        }
+        __syncthreads();
+        const int n = ctl[3];
+        // compressed Hessian entries and right-hand side, in parallel
+        for (int a = t; a < n; a += RED_NT) {
+          const int fa = idx[a];
+          L0[a] = d0[fa];                                            // M_aa
+          L1[a] = a >= 1 ? als_m_low(e1, e2, fa, idx[a - 1]) : 0.0;  // M_a,a-1
+          L2[a] = a >= 2 ? als_m_low(e1, e2, fa, idx[a - 2]) : 0.0;  // M_a,a-2
+          vz[a] = vb[fa];
+        }
+        __syncthreads();
+        if (t == 0) {
+          // banded LDLᵀ (unit L, bandwidth 2) fused with the forward solve L z = b, then
+          // x = L⁻ᵀ D⁻¹ z; the recurrences are carried in registers, one division per step
+          double dm1 = 1.0, dm2 = 1.0, im1 = 0.0, im2 = 0.0, l1m1 = 0.0, zm1 = 0.0, zm2 = 0.0;
           for (int a = 0; a < n; ++a) {
-            const int fa = idx[a];
-            double l2 = 0.0, l1 = 0.0;
-            if (a >= 2) l2 = als_m_low(e1, e2, fa, idx[a - 2]) / L0[a - 2];
-            if (a >= 1) l1 = (als_m_low(e1, e2, fa, idx[a - 1]) - (a >= 2 ? l2 * L1[a - 1] : 0.0)) / L0[a - 1];
-            L2[a] = l2;
+            const double m_aa = L0[a], m_a1 = L1[a], m_a2 = L2[a], b = vz[a];
+            const double l2 = m_a2 * im2;                              // l_{a,a-2}
+            const double l1 = (m_a1 - l2 * l1m1 * dm2) * im1;          // l_{a,a-1}
+            const double d = fmax(m_aa - l1 * l1 * dm1 - l2 * l2 * dm2, 1e-300);
+            const double id = 1.0 / d;
+            const double z = b - l1 * zm1 - l2 * zm2;
             L1[a] = l1;
-            L0[a] = sqrt(fmax(d0[fa] - l1 * l1 - l2 * l2, 1e-300));
+            L2[a] = l2;
+            vz[a] = z * id;  // y = D⁻¹ z
+            dm2 = dm1; dm1 = d; im2 = im1; im1 = id; l1m1 = l1; zm2 = zm1; zm1 = z;
           }
-          for (int a = 0; a < n; ++a) {
-            double z = vb[idx[a]];
-            if (a >= 1) z -= L1[a] * vz[a - 1];
-            if (a >= 2) z -= L2[a] * vz[a - 2];
-            vz[a] = z / L0[a];
-          }
+          double xp1 = 0.0, xp2 = 0.0, l1p1 = 0.0, l2p1 = 0.0, l2p2 = 0.0;
           for (int a = n - 1; a >= 0; --a) {
-            double x = vz[a];
-            if (a + 1 < n) x -= L1[a + 1] * vz[a + 1];
-            if (a + 2 < n) x -= L2[a + 2] * vz[a + 2];
-            vz[a] = x / L0[a];  // vz now holds x in compressed order
+            // x_a = y_a - l_{a+1,a} x_{a+1} - l_{a+2,a} x_{a+2}
+            const double x = vz[a] - l1p1 * xp1 - l2p2 * xp2;
+            vz[a] = x;
+            xp2 = xp1; xp1 = x;
+            l2p2 = l2p1; l2p1 = L2[a]; l1p1 = L1[a];
           }
-          for (int a = 0; a < n; ++a) vx[idx[a]] = vz[a];
           ctl[0] = 0;
           ctl[1] = -1;
         }
+        __syncthreads();
+        for (int a = t; a < n; a += RED_NT) vx[idx[a]] = vz[a];
         __syncthreads();
         for (int f = t; f < F; f += RED_NT) {
           const double x = vx[f];
@@ -2451,6 +2485,7 @@ static PassKernel make_pk_als() {
 // the constrained-ALS W-step pass (k <= 4): the VALU pass kernel with the ALS phase 2 and fp64 Ht
 template <typename TX>
 static bool pick_als_tx(int F, int np, PassKernel* out) {
+  if (F == 81 && np == 2) { *out = make_pk_als<TX, 81, 2, true>(); return true; }  // IOP grid (cfg5)
   if (np <= 1) { *out = make_pk_als<TX, 0, 1, true>(); return true; }
   if (np == 2) { *out = make_pk_als<TX, 0, 2, true>(); return true; }
   const int npw = (np + NWAVE - 1) / NWAVE;

@@ -1128,6 +1128,8 @@ __device__ __forceinline__ float dpp_add(float v) {
 
 // 16-byte chunk i of this thread for tile `tile`: X chunk (t + 256 i), or for i = 5 and t < 80 the
 // tail of X (t < 16) / the W tile (16 <= t < 80); threads t >= 80 re-read X chunk t (not stored).
+// LOADW = false (W resident in LDS): the W slots re-read X chunk t as well.
+template <bool LOADW = true>
 __device__ __forceinline__ void sl_prefetch(u32x4 (&pf)[PFN], const unsigned char* __restrict__ X,
                                             const unsigned char* __restrict__ W, int64_t tile, int t) {
   const unsigned char* xs = X + (size_t)tile * XB + 16 * t;
@@ -1135,15 +1137,16 @@ __device__ __forceinline__ void sl_prefetch(u32x4 (&pf)[PFN], const unsigned cha
   for (int i = 0; i < PFN - 1; ++i)
     pf[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xs + 4096 * i));
   const unsigned char* last = t < 16 ? xs + 4096 * (PFN - 1)
-                                     : (t < 80 ? W + (size_t)tile * WB + 16 * (t - 16) : xs);
+                                     : ((LOADW && t < 80) ? W + (size_t)tile * WB + 16 * (t - 16) : xs);
   pf[PFN - 1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(last));
 }
 
+template <bool STAGEW = true>
 __device__ __forceinline__ void sl_stage(unsigned char* smem, int wpar, const u32x4 (&pf)[PFN], int t) {
 #pragma unroll
   for (int i = 0; i < PFN - 1; ++i)
     *reinterpret_cast<u32x4*>(smem + L_X + 16 * t + 4096 * i) = pf[i];
-  if (t < 80) {
+  if (t < (STAGEW ? 80 : 16)) {
     unsigned char* dst = t < 16 ? smem + L_X + 16 * t + 4096 * (PFN - 1)
                                 : smem + L_W + wpar * WB + 16 * (t - 16);
     *reinterpret_cast<u32x4*>(dst) = pf[PFN - 1];
@@ -1189,8 +1192,10 @@ __device__ __forceinline__ void phase1(unsigned char* smem, float (&xv)[NC], int
 }
 
 // phase 2: lane = (sample 16w + lane/4, component lane%4): the MU update of w[s][j] in fp64
+// wres (W resident in LDS, mu_iter_sl_kernel<…, true>): this tile's W [64][4] is read from and
+// the new W written back to LDS; otherwise the staged tile is read and the new W stored to HBM.
 __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ W, int64_t tile, int wpar,
-                                       int wave, int lane, double l1, double l2) {
+                                       int wave, int lane, double l1, double l2, float* wres = nullptr) {
   const double* sP = reinterpret_cast<const double*>(smem + L_P);
   const double* sHHt = reinterpret_cast<const double*>(smem + L_HHT);
   float* sWn = reinterpret_cast<float*>(smem + L_WN);
@@ -1198,7 +1203,7 @@ __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ 
   const int j = lane & 3;
   const double num = (sP[(0 * TS + s) * K + j] + sP[(1 * TS + s) * K + j]) +
                      (sP[(2 * TS + s) * K + j] + sP[(3 * TS + s) * K + j]);
-  const float* sWo = reinterpret_cast<const float*>(smem + L_W + wpar * WB);
+  const float* sWo = wres ? wres : reinterpret_cast<const float*>(smem + L_W + wpar * WB);
   const float4 wv = *reinterpret_cast<const float4*>(sWo + s * K);
   const double wold = (double)sWo[s * K + j];
   const double* hr = sHHt + j * K;
@@ -1211,7 +1216,10 @@ __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ 
   if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
   if (den == 0.0) den = EPS32;          // SK:620
   const float wn = (float)(wold * (num / den));  // SK:622-629
-  W[((size_t)tile * TS + s) * K + j] = wn;
+  if (wres)
+    wres[s * K + j] = wn;  // the quad's float4 read above precedes this store (data dependence)
+  else
+    W[((size_t)tile * TS + s) * K + j] = wn;
   sWn[s * K + j] = wn;
 }
 
@@ -1837,19 +1845,33 @@ constexpr int TL_IT = 64, TL_WG = 2048;
 __device__ unsigned long long g_tl[TL_IT * TL_WG * 2];
 __device__ unsigned long long g_tl_pub[TL_IT];
 __device__ unsigned long long g_tl_start[TL_WG];
+__device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits), HW_REG_XCC_ID
 #define TL(it_, slot_)                                                                          \
   do {                                                                                          \
     if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define TL_PUB(it_) do { if (t == 0 && (it_) < TL_IT) g_tl_pub[it_] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define TL_START do { if (t == 0 && b < TL_WG) g_tl_start[b] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_START                                                                               \
+  do {                                                                                         \
+    if (t == 0 && b < TL_WG) {                                                                 \
+      g_tl_start[b] = __builtin_amdgcn_s_memrealtime();                                        \
+      unsigned hw_, xcc_;                                                                      \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));                        \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_));                      \
+      g_tl_hw[2 * b] = hw_;                                                                    \
+      g_tl_hw[2 * b + 1] = xcc_;                                                               \
+    }                                                                                          \
+  } while (0)
 #else
 #define TL(it_, slot_) do {} while (0)
 #define TL_PUB(it_) do {} while (0)
 #define TL_START do {} while (0)
 #endif
 
-template <int PD>
+// WRES: W stays resident in LDS for the whole launch (this workgroup's tiles, loaded once at the
+// start and written back once at the end): the passes stream only X, 324 instead of 356 bytes per
+// sample ("keep tensors resident instead of re-reading them").  Needs nbt·1 KB of extra LDS.
+template <int PD, bool WRES>
 __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(PersistArgs a) {
   using namespace sl;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1894,11 +1916,19 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
   const int nbt = (int)((a.n_tiles - b + G - 1) / G);
   const int total = a.n_iter * nbt;
   auto tile_at = [&](int q) -> int64_t { return b + (int64_t)G * (q % nbt); };
+  unsigned char* wres = smem + L_PTOTAL;  // [nbt][64][4] fp32 when WRES
+  if (WRES) {
+    for (int c = t; c < nbt * (WB / 16); c += NT) {
+      const int i = c / (WB / 16), ch = c - i * (WB / 16);
+      *reinterpret_cast<u32x4*>(wres + i * WB + 16 * ch) =
+          *reinterpret_cast<const u32x4*>(Wb + (size_t)(b + (int64_t)G * i) * WB + 16 * ch);
+    }
+  }
   u32x4 pfA[PFN], pfB[PFN];
-  sl_prefetch(pfA, Xb, Wb, tile_at(0), t);
-  if (PD == 2 && total > 1) sl_prefetch(pfB, Xb, Wb, tile_at(1), t);
-  sl_stage(smem, 0, pfA, t);
-  if (total > PD) sl_prefetch(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
+  sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(0), t);
+  if (PD == 2 && total > 1) sl_prefetch<!WRES>(pfB, Xb, Wb, tile_at(1), t);
+  sl_stage<!WRES>(smem, 0, pfA, t);
+  if (total > PD) sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
   lds_barrier();
   TL_START;
 
@@ -1916,11 +1946,12 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     phase1(smem, xv, wave, lane);
     // this wave's W store of the previous tile has landed (vmcnt retires in order; at most the 6
     // loads issued after it may remain) before any wave passes barrier A and prefetches W again
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (!WRES) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     lds_barrier();  // A
-    phase2(smem, a.W, tile, wpar, wave, lane, a.l1W, a.l2W);
-    if (has1) sl_stage(smem, wpar ^ 1, pf, t);
-    if (hasP && !end_it) sl_prefetch(pf, Xb, Wb, tile_at(q + 1 + PD), t);
+    phase2(smem, a.W, tile, wpar, wave, lane, a.l1W, a.l2W,
+           WRES ? reinterpret_cast<float*>(wres + i * WB) : nullptr);
+    if (has1) sl_stage<!WRES>(smem, wpar ^ 1, pf, t);
+    if (hasP && !end_it) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);
     lds_barrier();  // B
     phase3(smem, xv, acc, acc33, wave, lane);
     wpar ^= 1;
@@ -1936,7 +1967,7 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     acc33 = 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
     __syncthreads();
-    if (hasP) sl_prefetch(pf, Xb, Wb, tile_at(q + 1 + PD), t);  // in flight during the reduction
+    if (hasP) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);  // in flight during the reduction
     TL(it, 0);
     if (t == 0) {
       const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1966,6 +1997,13 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     const bool top = sFlag[1] != 0;
     if (last_it) {
       alive = false;
+      if (WRES) {  // this workgroup's W back to HBM, once per launch
+        for (int c = t; c < nbt * (WB / 16); c += NT) {
+          const int ii = c / (WB / 16), ch = c - ii * (WB / 16);
+          *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(b + (int64_t)G * ii) * WB + 16 * ch) =
+              *reinterpret_cast<const u32x4*>(wres + ii * WB + 16 * ch);
+        }
+      }
       if (!top) return;
       // the last combiner of the launch: every other workgroup has arrived for the last time
       if (a.apply_last) sl_update_basis(smem, t, a.l1H, a.l2H);
@@ -2203,7 +2241,11 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
             const double l2 = m_a2 * im2;                              // l_{a,a-2}
             const double l1 = (m_a1 - l2 * l1m1 * dm2) * im1;          // l_{a,a-1}
             const double d = fmax(m_aa - l1 * l1 * dm1 - l2 * l2 * dm2, 1e-300);
-            const double id = 1.0 / d;
+            // 1/d: v_rcp_f64 refined by two Newton steps (full fp64 accuracy) — the IEEE division
+            // sequence sat on this loop's critical path
+            double id = __builtin_amdgcn_rcp(d);
+            id = fma(id, fma(-d, id, 1.0), id);
+            id = fma(id, fma(-d, id, 1.0), id);
             const double z = b - l1 * zm1 - l2 * zm2;
             L1[a] = l1;
             L2[a] = l2;
@@ -2929,6 +2971,7 @@ int cnmf_debug_timeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl), sizeof(unsigned long long) * TL_IT * TL_WG * 2));
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2, HIP_SYMBOL(g_tl_pub), sizeof(unsigned long long) * TL_IT));
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2 + TL_IT, HIP_SYMBOL(g_tl_start), sizeof(unsigned long long) * TL_WG));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2 + TL_IT + TL_WG, HIP_SYMBOL(g_tl_hw), sizeof(unsigned int) * TL_WG * 2));
   return CNMF_OK;
 }
 int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
@@ -2955,11 +2998,13 @@ int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, vo
 // The persistent path serves fp32 X at F = 81, k = 4 with whole tiles and >= 3 tiles per workgroup
 // (CNMF_PERSIST=0 disables it for A/B timing).  Returns its grid, 0 when not eligible, < 0 on error.
 static bool g_no_persist = getenv("CNMF_PERSIST") && strcmp(getenv("CNMF_PERSIST"), "0") == 0;
-// prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2)
+// prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2); CNMF_WRES=0 keeps W streaming
 static int g_persist_pd = (getenv("CNMF_PERSIST_PD") && atoi(getenv("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
-static PassFn persist_fn() {
-  return g_persist_pd == 1 ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1>)
-                           : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2>);
+static bool g_no_wres = getenv("CNMF_WRES") && strcmp(getenv("CNMF_WRES"), "0") == 0;
+static PassFn persist_fn(bool wres = false) {
+  if (g_persist_pd == 1)
+    return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, false>);
+  return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, false>);
 }
 
 static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k) {
@@ -2976,6 +3021,17 @@ static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k) {
   int64_t G = std::min<int64_t>({maxb, rows_cap, n_tiles / min_tiles, (int64_t)sl::GROUP * sl::MAX_GROUPS});
   const int64_t rounds = (n_tiles + G - 1) / G;
   return (n_tiles + rounds - 1) / rounds;  // <= G, so every workgroup still owns >= min_tiles
+}
+
+// LDS of the W-resident variant for this grid, or 0 when it would lower the residency
+static size_t persist_wres_lds(int64_t n_rows, int64_t G) {
+  if (g_no_wres || G <= 0) return 0;
+  const int64_t nbt_max = (n_rows / TS + G - 1) / G;
+  const size_t lds = (size_t)sl::L_PTOTAL + (size_t)nbt_max * sl::WB;
+  if (lds > kMaxLds) return 0;
+  const int64_t base = max_resident(persist_fn(false), sl::L_PTOTAL);
+  const int64_t with = max_resident(persist_fn(true), lds);
+  return (with > 0 && with >= base) ? lds : 0;
 }
 
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
@@ -3013,11 +3069,15 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
   void* args[] = {&pa};
+  const size_t wlds = n_iter > 1 ? persist_wres_lds(n_rows, G) : 0;
   // a plain launch: the grid is at most the occupancy query's co-resident capacity (persist_grid;
   // 106 SGPRs admit 6 workgroups per CU by MI355X_MICROARCH.md's residency formula, we use 2) and
   // every wait in the kernel is bounded, so a short residency ends in the error word, not a hang.
   // (hipLaunchCooperativeKernel made rocprofv3 crash at process exit and costs ~17 us per launch.)
-  HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, s));
+  if (wlds)
+    HIP_CHECK(hipLaunchKernel(persist_fn(true), dim3((unsigned)G), dim3(NT), args, wlds, s));
+  else
+    HIP_CHECK(hipLaunchKernel(persist_fn(false), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, s));
   return CNMF_OK;
 }
 

@@ -46,13 +46,14 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     launch_us = e0.elapsed_time(e1) * 1e3
-    buf = np.zeros(TL_IT * TL_WG * 2 + TL_IT + TL_WG, dtype=np.uint64)
+    buf = np.zeros(TL_IT * TL_WG * 2 + TL_IT + TL_WG + TL_WG, dtype=np.uint64)
     _lib.check(fn(buf.ctypes.data), "timeline")
     G = plan.n_parts
     from cnmf_amd.solver import MUPlan as _M  # noqa: F401
     tl = buf[:TL_IT * TL_WG * 2].reshape(TL_IT, TL_WG, 2).astype(np.int64)
     pub = buf[TL_IT * TL_WG * 2:TL_IT * TL_WG * 2 + TL_IT].astype(np.int64)
-    start = buf[TL_IT * TL_WG * 2 + TL_IT:].astype(np.int64)
+    start = buf[TL_IT * TL_WG * 2 + TL_IT:TL_IT * TL_WG * 2 + TL_IT + TL_WG].astype(np.int64)
+    hw = buf[TL_IT * TL_WG * 2 + TL_IT + TL_WG:].view(np.uint32).reshape(TL_WG, 2)
     # the grid actually launched: workgroups with a start stamp in this launch
     g = int(np.count_nonzero(start[:G] >= start[:G].max() - 10_000_000))
     n = min(a.iters, TL_IT)
@@ -84,6 +85,24 @@ def main():
                     "stream_by_tiles": {int(v): round(float(mean_wg[nbt == v].mean()), 2) for v in np.unique(nbt)},
                     "per_wg_mean_min_max": [round(float(mean_wg.min()), 2), round(float(mean_wg.max()), 2)],
                     "within_wg_std_us": round(float(spans.std(axis=0).mean()), 2)})
+    # physical placement: HW_ID bits cu_id [11:8], sh_id [12], se_id [15:13]; XCC_ID [3:0]
+    hwid, xcc = hw[:g, 0].astype(np.int64), hw[:g, 1].astype(np.int64) & 0xF
+    cu = (hwid >> 8) & 0xF
+    se = (hwid >> 13) & 0x7
+    sh = (hwid >> 12) & 0x1
+    key = xcc * 1000 + se * 100 + sh * 16 + cu
+    uk, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    per_cu = np.bincount(inv, weights=mean_wg) / cnt
+    co = cnt[inv]  # workgroups sharing this block's CU
+    summary.update({"n_cus_used": int(len(uk)), "wgs_per_cu_hist": {int(c): int((cnt == c).sum()) for c in np.unique(cnt)},
+                    "stream_by_wgs_on_cu": {int(c): round(float(mean_wg[co == c].mean()), 2) for c in np.unique(co)},
+                    "stream_by_xcc": [round(float(mean_wg[xcc == x].mean()), 2) for x in range(8)],
+                    "stream_by_se": [round(float(mean_wg[se == x].mean()), 2) if (se == x).any() else None for x in range(8)],
+                    "cu_mean_min_max": [round(float(per_cu.min()), 2), round(float(per_cu.max()), 2)],
+                    "same_cu_pair_corr": round(float(np.corrcoef(mean_wg, per_cu[inv])[0, 1]), 3),
+                    "b_mod_8_equals_xcc_frac": round(float(np.mean((np.arange(g) % 8) == xcc)), 3)})
+    slow = np.argsort(mean_wg)[-8:]
+    summary["slowest_wgs"] = [(int(b), int(xcc[b]), int(se[b]), int(cu[b]), round(float(mean_wg[b]), 1)) for b in slow]
     summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
                     "us_per_iter": round(launch_us / a.iters, 2),
                     "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})

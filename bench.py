@@ -2,8 +2,10 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python bench.py --solver als            # cfg5, the constrained ALS
+    python bench.py --features 300 --k 16 --dtype bf16   # cfg4, the bf16 matrix-core pass
 
-One "step" = one MU iteration (fused sample pass over X and W + reduction + basis update) on
+One "step" = one MU iteration (sample pass over X + cross-workgroup reduction + basis update) on
 synthetic IOP spectra (cnmf_amd.synthetic), V = 1e6 x 81 per GPU, k = 4, fp32, tol = 0, inputs
 resident in HBM before the timed region.  Multi-GPU is weak scaling: each rank owns a 1e6-row shard
 and the k·(F+k) fp64 accumulators are all-reduced once per iteration (RCCL, backend "nccl").
@@ -11,9 +13,10 @@ and the k·(F+k) fp64 accumulators are all-reduced once per iteration (RCCL, bac
 value = sum over ranks of (shard rows / 1e6) × iterations / wall seconds, i.e. MU iterations per
 second on a 1e6 x 81 problem (exactly it/s at N = 1; the whole-job aggregate at N > 1).
 
-Extra keys: roofline (dominant kernel = mu_pass_kernel, per-launch HIP-event timing inside the timed
-region on the launch stream; algorithmic bytes = N·(F·4 + 2·k·4) per launch), cpu_baseline (the
-NumPy oracle, rank 0 at N = 1 only, bounded sample), parity (small fixed-size check vs the oracle).
+Extra keys: roofline (the dominant kernel timed with HIP events on its launch stream inside the
+timed region: at N = 1 the ONE persistent launch that runs all K iterations, else each per-iteration
+launch; achieved = algorithmic bytes N·(F·4 + 2·k·4) per iteration × iterations per launch ÷ launch
+time), cpu_baseline (the NumPy / scipy oracle, rank 0 at N = 1 only, bounded sample).
 """
 from __future__ import annotations
 
@@ -35,7 +38,10 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=500)
-    p.add_argument("--warmup", type=int, default=20)
+    # 1000 warmup iterations (~70 ms at cfg2): after idle the chip runs its first ~35 ms of work at
+    # lower clocks (tools/bench_trend.py: 73.7 us/iteration on the first 500-iteration launch,
+    # 66 us on the following ones), so a short warmup would time the clock ramp, not the solver
+    p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
     p.add_argument("--features", type=int, default=81)
     p.add_argument("--k", type=int, default=4)

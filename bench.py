@@ -52,6 +52,9 @@ def parse():
                    help="mu: cfg2 (the headline); als: cfg5, the constrained ALS")
     p.add_argument("--sum-to-one", type=float, default=1.0, help="ALS sum-to-one weight (delta)")
     p.add_argument("--smoothness", type=float, default=0.5, help="ALS smoothness penalty (lambda)")
+    p.add_argument("--dist", action="store_true",
+                   help="use the multi-GPU code path (shard step + RCCL all_reduce per iteration) "
+                        "even at one rank (diagnostic; a world-size-1 nccl group)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
@@ -137,7 +140,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if args.dist and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    dist_path = world > 1 or args.dist
+    if dist_path:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -163,6 +172,8 @@ def main():
         plan = MUPlan(Xd, k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
+    if args.dist and args.solver == "mu":
+        plan.use_shard_steps()
     torch.cuda.synchronize()
 
     plan.iterate(args.warmup)
@@ -275,7 +286,7 @@ def main():
         "data": "synthetic",
         "config": {"workload": workload,
                    "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
-                   "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64)"},
+                   "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64)" + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else "")},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

@@ -85,9 +85,16 @@ class MUPlan:
             p = self.lib.cnmf_mu_persistent(self.n_rows, self.F, self.k, self.xdt)
         self.persistent_shape = bool(check(p, "cnmf_mu_persistent"))  # the persistent kernel serves it
         self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
+        self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
         self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)
+
+    def use_shard_steps(self):
+        """Run the multi-GPU iteration (one shard step + one all_reduce per iteration) even on a
+        single rank — a diagnostic of that path's per-iteration cost."""
+        self.shard_steps = True
+        self.persistent = False
 
     # -- plumbing ------------------------------------------------------------------------------
     def _stream(self):
@@ -136,7 +143,8 @@ class MUPlan:
                 self.l2_H, int(apply_first), self._stream()), "cnmf_mu_shard_step")
 
     def _allreduce(self, t: torch.Tensor):
-        if self.world > 1:
+        if self.world > 1 or (self.shard_steps and torch.distributed.is_available()
+                              and torch.distributed.is_initialized()):
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
     def check_sync_error(self):
@@ -157,7 +165,7 @@ class MUPlan:
             for _ in range(n_iter):  # transform: W only, H (and Ht/HHt) fixed (SK:854 skipped)
                 self.sample_pass(_lib.PASS_UPDATE_W)
             return
-        if self.world == 1:
+        if self.world == 1 and not self.shard_steps:
             with torch.cuda.device(self.device):
                 check(self.lib.cnmf_mu_iterations(
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),

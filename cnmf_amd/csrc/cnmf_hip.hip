@@ -1287,6 +1287,145 @@ __device__ __forceinline__ void flush_acc(float* red, float (&acc)[NC][K], float
 }
 }  // namespace sl
 
+// ------------------------------------------------------------------------------------------------
+// The constrained-ALS W-step on the sample-lane layout (cfg5: fp32 X, F = 81, k = 4, full tiles):
+// phase 1 forms c = Hx in fp64 (lane = sample, wave = 21 features, Hᵀ in fp64 in LDS; the solve
+// amplifies errors by cond(Q), so no fp32 chains here), phase 2 is the exact FCLS of phase12's
+// ALS branch (lane = (sample, component): the 16 passive sets, 4 per lane, least objective by quad
+// shuffles; oracle/als_ref.py), phase 3 the sl accumulation of [WᵀX | WᵀW] (SK:639-640 form).
+// ------------------------------------------------------------------------------------------------
+namespace sl {
+constexpr int L_HT64 = (L_TOTAL + 15) / 16 * 16;      // Hᵀ fp64 [84][4] (rows >= 81 zero)
+constexpr int L_TAB = L_HT64 + NWAVE * NF * K * 8;     // passive-set table (ALS_TAB doubles)
+constexpr int L_ALS_TOTAL = L_TAB + ALS_TAB * 8;
+}  // namespace sl
+
+__global__ __launch_bounds__(NT, 2) void als_pass_sl_kernel(const float* __restrict__ X,
+                                                           float* __restrict__ W,
+                                                           const double* __restrict__ Ht,
+                                                           const double* __restrict__ table,
+                                                           double* __restrict__ partials,
+                                                           int64_t n_tiles, double delta2,
+                                                           int64_t n_rows_out) {
+  using namespace sl;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(X);
+  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(W);
+  double* sHt = reinterpret_cast<double*>(smem + L_HT64);
+  double* sTab = reinterpret_cast<double*>(smem + L_TAB);
+  double* sP = reinterpret_cast<double*>(smem + L_P);
+  float* sWn = reinterpret_cast<float*>(smem + L_WN);
+
+  for (int e = t; e < NWAVE * NF * K; e += NT) sHt[e] = e < F * K ? Ht[e] : 0.0;
+  for (int e = t; e < ALS_TAB; e += NT) sTab[e] = table[e];
+  if (t < 4) reinterpret_cast<float*>(smem + L_X + XB)[t] = 0.f;
+
+  float acc[NC][K];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int j = 0; j < K; ++j) acc[c][j] = 0.f;
+  float acc33 = 0.f;
+
+  const int64_t G = gridDim.x;
+  int64_t tile = blockIdx.x;
+  u32x4 pf[PFN];
+  sl_prefetch(pf, Xb, Wb, tile, t);
+  sl_stage(smem, 0, pf, t);
+  if (tile + G < n_tiles) sl_prefetch(pf, Xb, Wb, tile + G, t);
+  lds_barrier();
+
+  int wpar = 0;
+  for (; tile < n_tiles; tile += G, wpar ^= 1) {
+    // ---- phase 1: c partials in fp64 (lane = sample, wave = 21 features)
+    float xv[NC];
+    {
+      const float* xr = reinterpret_cast<const float*>(smem + L_X) + lane * F + NF * wave;
+#pragma unroll
+      for (int c = 0; c < NF; ++c) xv[c] = xr[c];
+      double p[K] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < NF; ++c) {
+        const double* h = sHt + (NF * wave + c) * K;
+        const double2 h01 = *reinterpret_cast<const double2*>(h);
+        const double2 h23 = *reinterpret_cast<const double2*>(h + 2);
+        const double x = (double)xv[c];
+        p[0] = fma(x, h01.x, p[0]);
+        p[1] = fma(x, h01.y, p[1]);
+        p[2] = fma(x, h23.x, p[2]);
+        p[3] = fma(x, h23.y, p[3]);
+      }
+      double* pw = sP + ((size_t)wave * TS + lane) * K;
+      *reinterpret_cast<double2*>(pw) = make_double2(p[0], p[1]);
+      *reinterpret_cast<double2*>(pw + 2) = make_double2(p[2], p[3]);
+    }
+    lds_barrier();  // A
+    // ---- phase 2: exact FCLS per sample, lane = (sample 16w + lane/4, component lane%4)
+    {
+      const int s = 16 * wave + (lane >> 2);
+      const int qtr = lane & 3;
+      double c[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        c[j] = ((sP[(0 * TS + s) * K + j] + sP[(1 * TS + s) * K + j]) +
+                (sP[(2 * TS + s) * K + j] + sP[(3 * TS + s) * K + j])) + delta2;
+      double bestf = 1.0;
+      int bestm = 16;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int m = qtr + 4 * u;
+        const double* T = sTab + m * 16;
+        bool feas = sTab[256 + m] != 0.0;
+        double f = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          double v = 0.0;
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) v = fma(T[r * 4 + cc], c[cc], v);
+          feas = feas && v >= 0.0;
+          f = fma(c[r], v, f);
+        }
+        f *= -0.5;
+        if (feas && (f < bestf || (f == bestf && m < bestm))) {
+          bestf = f;
+          bestm = m;
+        }
+      }
+#pragma unroll
+      for (int off = 1; off <= 2; off <<= 1) {
+        const double of = __shfl_xor(bestf, off);
+        const int om = __shfl_xor(bestm, off);
+        if (of < bestf || (of == bestf && om < bestm)) {
+          bestf = of;
+          bestm = om;
+        }
+      }
+      const double* T = sTab + min(bestm, 15) * 16;
+      double wn64 = 0.0;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) wn64 = fma(T[qtr * 4 + cc], c[cc], wn64);
+      const float wn = (float)fmax(wn64, 0.0);
+      W[((size_t)tile * TS + s) * K + qtr] = wn;
+      sWn[s * K + qtr] = wn;
+    }
+    if (tile + G < n_tiles) {
+      sl_stage(smem, wpar ^ 1, pf, t);
+      if (tile + 2 * G < n_tiles) sl_prefetch(pf, Xb, Wb, tile + 2 * G, t);
+    }
+    lds_barrier();  // B
+    phase3(smem, xv, acc, acc33, wave, lane);
+  }
+  lds_barrier();
+  flush_acc<false>(reinterpret_cast<float*>(smem + L_X), acc, acc33,
+                   partials + (size_t)blockIdx.x * (K * V), wave, lane, t);
+  // partial rows beyond this grid (the caller's row count is the sl grid) are zero
+  for (int64_t r = blockIdx.x + G; r < n_rows_out; r += G)
+    for (int e = t; e < K * V; e += NT) partials[(size_t)r * (K * V) + e] = 0.0;
+}
+
 __global__ __launch_bounds__(NT, 3) void mu_pass_sl_kernel(const float* __restrict__ X,
                                                           float* __restrict__ W,
                                                           const double* __restrict__ Ht,
@@ -2926,6 +3065,31 @@ int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, 
   const int64_t nb = main_grid(n_rows, x_dtype, n_features, k, &pmain, &lmain);  // = partial rows
   if (nb < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (nb == 0) return CNMF_OK;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  int64_t als_rows = n_rows;
+  int64_t row0 = 0, part0 = 0;
+  if (accumulate && use_sl(x_dtype, n_features, k)) {
+    // the sample-lane ALS pass on the full tiles (its grid = the sl grid = the first partial rows),
+    // the ragged tail (< 64 rows) on one workgroup of the VALU ALS pass (partial row g)
+    int64_t n_full;
+    bool tail;
+    const int64_t g = sl_grid(n_rows, &n_full, &tail);
+    if (g < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+    if (g > 0) {
+      // its own rounds-balanced grid (2 workgroups per CU), <= g; it zeroes partial rows [ga, g)
+      const int64_t ga = std::min<int64_t>(
+          g, pass_grid(n_full * TS, reinterpret_cast<PassFn>(&als_pass_sl_kernel), sl::L_ALS_TOTAL));
+      if (ga <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+      hipLaunchKernelGGL(als_pass_sl_kernel, dim3((unsigned)ga), dim3(NT), sl::L_ALS_TOTAL, hs,
+                         static_cast<const float*>(X), static_cast<float*>(W), Ht, table, partials,
+                         n_full, sum_to_one * sum_to_one, g);
+      HIP_CHECK(hipGetLastError());
+    }
+    if (!tail) return CNMF_OK;
+    row0 = n_full * TS;
+    part0 = g;
+    als_rows = n_rows - row0;
+  }
   PassKernel pk;
   const int np = (n_features + k + 63) / 64;
   bool ok = false;
@@ -2941,9 +3105,13 @@ int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, 
   int F = n_features;
   int flags = CNMF_PASS_UPDATE_W | (accumulate ? CNMF_PASS_ACCUMULATE : 0);
   double d2 = sum_to_one * sum_to_one, zero = 0.0;
-  const int64_t n_tiles = (n_rows + TS - 1) / TS;
-  void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&table, &partials, &n_rows, &F, &k, &d2, &zero, &flags, (void*)&n_tiles};
-  HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)nb), dim3(NT), args, lds, reinterpret_cast<hipStream_t>(stream)));
+  const int64_t n_tiles = (als_rows + TS - 1) / TS;
+  const void* Xr = static_cast<const unsigned char*>(X) + row0 * F * (int64_t)pk.sx;
+  void* Wr = static_cast<unsigned char*>(W) + row0 * k * (int64_t)pk.sc;
+  double* pr = partials ? partials + part0 * (int64_t)k * (F + k) : nullptr;
+  const int64_t grid = row0 > 0 ? 1 : nb;
+  void* args[] = {(void*)&Xr, &Wr, (void*)&Ht, (void*)&table, &pr, &als_rows, &F, &k, &d2, &zero, &flags, (void*)&n_tiles};
+  HIP_CHECK(hipLaunchKernel(pk.fn, dim3((unsigned)grid), dim3(NT), args, lds, hs));
   return CNMF_OK;
 }
 

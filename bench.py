@@ -53,8 +53,13 @@ def parse():
     p.add_argument("--sum-to-one", type=float, default=1.0, help="ALS sum-to-one weight (delta)")
     p.add_argument("--smoothness", type=float, default=0.5, help="ALS smoothness penalty (lambda)")
     p.add_argument("--dist", action="store_true",
-                   help="use the multi-GPU code path (shard step + RCCL all_reduce per iteration) "
-                        "even at one rank (diagnostic; a world-size-1 nccl group)")
+                   help="use the multi-GPU code path even at one rank (diagnostic; a world-size-1 "
+                        "nccl group): the in-launch exchange with itself, or with --exchange off "
+                        "shard step + RCCL all_reduce per iteration")
+    p.add_argument("--exchange", default="auto", choices=["auto", "off"],
+                   help="multi-GPU MU: auto = the all-reduce inside the persistent launch (peer "
+                        "exchange over xGMI), validated against the RCCL path before timing and "
+                        "replaced by it on any failure; off = shard step + RCCL all_reduce")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
@@ -117,6 +122,53 @@ def cpu_baseline_als(X, W0, H0, delta, lam, budget_s):
             "seconds": round(el, 3)}
 
 
+def validate_exchange(plan, W0, H0d, n=20):
+    """Set up the in-launch exchange and check it against the RCCL path from the same start:
+    n iterations each way; every rank must end with bit-identical H, both paths must agree to fp64
+    summation-order noise, and no launch may report an error.  Leaves the plan at (W0, H0) on the
+    path to time.  Returns a status string."""
+    import torch
+    import torch.distributed as dist
+    dev = plan.device
+    try:
+        plan.enable_exchange()
+    except Exception as e:  # every rank raises together (enable_exchange agrees collectively)
+        return f"unavailable ({str(e)[:300]}); RCCL path timed"
+    fail, why = 0.0, ""
+    try:
+        plan.iterate(n)
+        torch.cuda.synchronize()
+        plan.check_sync_error()
+    except Exception as e:
+        fail, why = 1.0, str(e)[:200]
+    Hx, Wx = plan.H64.clone(), plan.W.clone()
+    xgen = plan.xgen
+    plan.exchange, plan.persistent = False, False
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(H0d)
+    plan.iterate(n)  # shard steps + RCCL all_reduce
+    torch.cuda.synchronize()
+    dH = float((Hx - plan.H64).norm() / plan.H64.norm())
+    dW = float((Wx.double() - plan.W.double()).norm() / plan.W.double().norm())
+    hmax, hmin = Hx.clone(), Hx.clone()
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    same = bool(torch.equal(hmax, hmin))
+    bad = fail or (not same) or not (dH < 1e-9 and dW < 1e-5)
+    st = torch.tensor([1.0 if bad else 0.0, dH, dW], dtype=torch.float64, device=dev)
+    dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(H0d)
+    torch.cuda.synchronize()
+    if float(st[0]) != 0.0:
+        plan.disable_exchange()
+        return (f"failed validation (error: {why or 'none'}, ranks identical: {same}, rel diff vs "
+                f"RCCL path H {float(st[1]):.2e} W {float(st[2]):.2e}); RCCL path timed")
+    plan.exchange, plan.persistent, plan.xgen = True, True, xgen
+    return (f"validated over {n} iterations: H identical on all ranks, rel diff vs the RCCL path "
+            f"H {float(st[1]):.2e} W {float(st[2]):.2e}")
+
+
 def load_traffic(path, n_rows, F, k):
     """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py)."""
     try:
@@ -172,31 +224,70 @@ def main():
         plan = MUPlan(Xd, k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
-    if args.dist and args.solver == "mu":
+    exchange = None
+    if args.solver == "mu" and dist_path and args.exchange == "auto" and plan.persistent_shape:
+        exchange = validate_exchange(plan, W0, H0d)
+        print(f"[rank {rank}] in-launch exchange: {exchange}", file=sys.stderr, flush=True)
+    elif args.dist and args.solver == "mu":
         plan.use_shard_steps()
     torch.cuda.synchronize()
 
     plan.iterate(args.warmup)
     torch.cuda.synchronize()
+    if plan.exchange:  # a failed warmup launch falls back before anything is timed
+        fail = torch.zeros(1, dtype=torch.float64, device=dev)
+        try:
+            plan.check_sync_error()
+        except Exception as e:
+            fail[0] = 1.0
+            print(f"[rank {rank}] exchange warmup failed: {e}", file=sys.stderr, flush=True)
+        dist.all_reduce(fail, op=dist.ReduceOp.MAX)
+        if float(fail[0]) != 0.0:
+            plan.disable_exchange()
+            exchange = "failed in warmup; RCCL path timed"
+            plan.set_W(torch.from_numpy(W0))
+            plan.set_H(H0d)
+            plan.iterate(args.warmup)
+            torch.cuda.synchronize()
 
     K = args.steps
-    persistent = world == 1 and plan.persistent
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if persistent else 2 * K)]
-    stream = torch.cuda.current_stream(dev)
-    for e in events:  # creates the HIP events (outside the timed region)
-        e.record(stream)
-    torch.cuda.synchronize()
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    plan.iterate(K, pass_events=events)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    def timed():
+        persistent = plan.persistent and (world == 1 or plan.exchange)
+        events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if persistent else 2 * K)]
+        stream = torch.cuda.current_stream(dev)
+        for e in events:  # creates the HIP events (outside the timed region)
+            e.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        plan.iterate(K, pass_events=events)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        return persistent, events, elapsed
+
+    persistent, events, elapsed = timed()
+    if plan.exchange:  # a failed exchange launch: every rank re-times on RCCL
+        fail = torch.zeros(1, dtype=torch.float64, device=dev)
+        try:
+            plan.check_sync_error()
+        except Exception as e:
+            fail[0] = 1.0
+            print(f"[rank {rank}] exchange launch failed: {e}", file=sys.stderr, flush=True)
+        dist.all_reduce(fail, op=dist.ReduceOp.MAX)
+        if float(fail[0]) != 0.0:
+            plan.disable_exchange()
+            exchange = "failed in the timed launch; RCCL path re-timed"
+            plan.set_W(torch.from_numpy(W0))
+            plan.set_H(H0d)
+            plan.iterate(args.warmup)
+            torch.cuda.synchronize()
+            persistent, events, elapsed = timed()
     plan.check_sync_error()
     if persistent:  # ONE launch ran all K iterations (pass + in-launch reduction + basis update)
         launches = 1
@@ -233,9 +324,12 @@ def main():
         traffic = traffic * iters_per_launch
     if args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
-    elif persistent:
+    elif persistent and world == 1:
         kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
                  "update per launch)")
+    elif persistent:
+        kname = ("mu_iter_sl_kernel<..., MULTI> (persistent, one launch per rank: K iterations of "
+                 "pass + in-launch reduction + peer all-reduce over xGMI + basis update)")
     elif plan.persistent_shape:
         kname = ("mu_iter_sl_kernel shard step (one iteration per launch: pending basis update, "
                  "pass, in-launch reduction; all_reduce between launches)")
@@ -286,7 +380,10 @@ def main():
         "data": "synthetic",
         "config": {"workload": workload,
                    "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
-                   "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64)" + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else "")},
+                   "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64"
+                                  + (", in-launch over xGMI)" if plan.exchange else ", RCCL)")
+                                  + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
+                   "exchange": exchange},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

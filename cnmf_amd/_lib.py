@@ -67,6 +67,15 @@ _SIGS = {
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                   _i32, _f64, _f64, _f64, _f64, _i32, _vp]),
+    "cnmf_xbuf_bytes": (_i64, [_i32]),
+    "cnmf_xbuf_handle_bytes": (_i32, []),
+    "cnmf_xbuf_alloc": (_i32, [_i32, ctypes.POINTER(_vp), _vp]),
+    "cnmf_xbuf_open": (_i32, [_vp, ctypes.POINTER(_vp)]),
+    "cnmf_xbuf_close": (_i32, [_vp]),
+    "cnmf_xbuf_free": (_i32, [_vp]),
+    "cnmf_mu_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                        _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _i32,
+                                        ctypes.c_uint32, _vp, _i32, _vp]),
 }
 
 

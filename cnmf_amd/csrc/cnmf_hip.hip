@@ -1848,6 +1848,7 @@ constexpr int L_FLAG = L_AB + K * V * 8;                // 4 ints
 constexpr int L_PTOTAL = L_FLAG + 16;
 constexpr int GROUP = 16;                               // workgroups per first-level group
 constexpr int MAX_GROUPS = 64;
+constexpr uint32_t XPOISON = 0xFFFFFFFFu;                // exchange flag of a failed rank
 constexpr uint64_t SPIN_TIMEOUT = 200000000ull;         // 2 s of s_memrealtime (100 MHz)
 }  // namespace sl
 
@@ -1933,6 +1934,13 @@ struct PersistArgs {
   double l1W, l2W, l1H, l2H;
   int apply_first;   // first apply the pending basis update from AB (multi-GPU: AB all-reduced)
   int apply_last;    // apply the last iteration's basis update in-launch (single GPU)
+  // MULTI (one persistent launch per rank, the all-reduce in-launch): every rank's exchange buffer
+  // (fine-grained, IPC-mapped): slots [world][K*V] doubles, then one flag per source rank at 64-B
+  // strides (xflag_off bytes in); flags carry gen0 + it + 1 (monotonic across launches)
+  double* const* peers;
+  int rank, world;
+  uint32_t gen0;
+  int xflag_off;
 };
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -1983,6 +1991,7 @@ __device__ __forceinline__ void sum_rows_sc1(const double* rows, int m0, int ste
 constexpr int TL_IT = 64, TL_WG = 2048;
 __device__ unsigned long long g_tl[TL_IT * TL_WG * 2];
 __device__ unsigned long long g_tl_pub[TL_IT];
+__device__ unsigned long long g_tl_x[TL_IT * 4];  // MULTI exchange: start, stored, flags seen, summed
 __device__ unsigned long long g_tl_start[TL_WG];
 __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits), HW_REG_XCC_ID
 #define TL(it_, slot_)                                                                          \
@@ -1990,6 +1999,7 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
     if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define TL_PUB(it_) do { if (t == 0 && (it_) < TL_IT) g_tl_pub[it_] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_X(it_, slot_) do { if (t == 0 && (it_) < TL_IT) g_tl_x[(it_) * 4 + (slot_)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_START                                                                               \
   do {                                                                                         \
     if (t == 0 && b < TL_WG) {                                                                 \
@@ -2004,13 +2014,14 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
 #else
 #define TL(it_, slot_) do {} while (0)
 #define TL_PUB(it_) do {} while (0)
+#define TL_X(it_, slot_) do {} while (0)
 #define TL_START do {} while (0)
 #endif
 
 // WRES: W stays resident in LDS for the whole launch (this workgroup's tiles, loaded once at the
 // start and written back once at the end): the passes stream only X, 324 instead of 356 bytes per
 // sample ("keep tensors resident instead of re-reading them").  Needs nbt·1 KB of extra LDS.
-template <int PD, bool WRES>
+template <int PD, bool WRES, bool MULTI = false>
 __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(PersistArgs a) {
   using namespace sl;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -2126,6 +2137,63 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) {
+          // ---- the cross-rank all-reduce of AB (k(F+k) fp64), inside the launch: this rank's AB
+          // into slot `rank` of every rank's exchange buffer (remote stores over xGMI, system
+          // scope), a system-scope release, one flag per destination; then wait for every rank's
+          // flag in this rank's buffer and sum the slots in rank order (the same AB, bit for bit,
+          // on every rank).  Slots alternate by generation parity: a rank writes generation g+2
+          // only after it has seen every rank's flag g+1, which each rank raises only after it
+          // has read its generation-g slots.  A rank whose launch has failed raises XPOISON
+          // instead, which makes every peer fail too (no rank waits out its timeout per iteration).
+          constexpr int n_out = K * V;
+          const uint32_t gen = a.gen0 + (uint32_t)it + 1u;
+          TL_X(it, 0);
+          const size_t par = (size_t)(gen & 1u) * a.world * n_out;
+          for (int pr = 0; pr < a.world; ++pr) {
+            double* dst = a.peers[pr] + par + (size_t)a.rank * n_out;
+            for (int e = t; e < n_out; e += NT)
+              __hip_atomic_store(dst + e, sAB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          // every slot store is a system-scope atomic to fine-grained memory: once vmcnt(0) says
+          // it is acknowledged it is visible to every agent, so the flag can follow without a
+          // release fence (whose L2 writeback, buffer_wbl2, would stall this XCD for microseconds)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __syncthreads();
+          TL_X(it, 1);
+          if (t < a.world) {
+            const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+            uint32_t* f = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(a.peers[t]) +
+                                                      a.xflag_off + 64 * a.rank);
+            __hip_atomic_store(f, bad ? XPOISON : gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t* mf = reinterpret_cast<const uint32_t*>(
+                reinterpret_cast<const unsigned char*>(a.peers[a.rank]) + a.xflag_off + 64 * t);
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            uint32_t v;
+            while ((v = __hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < gen) {
+              if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+              if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
+                __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (v == XPOISON) __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          // no acquire fence either: the slot loads below are system-scope atomics (they bypass
+          // the caches) issued only after the flag value has come back
+          __syncthreads();
+          TL_X(it, 2);
+          const double* mine = a.peers[a.rank] + par;
+          for (int e = t; e < n_out; e += NT) {
+            double v = 0.0;
+            for (int q = 0; q < a.world; ++q)
+              v += __hip_atomic_load(mine + (size_t)q * n_out + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            sAB[e] = v;
+            st_sc1(a.AB + e, v);
+          }
+          TL_X(it, 3);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0 && !last_it)
@@ -3142,6 +3210,10 @@ int cnmf_debug_timeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2 + TL_IT + TL_WG, HIP_SYMBOL(g_tl_hw), sizeof(unsigned int) * TL_WG * 2));
   return CNMF_OK;
 }
+int cnmf_debug_xtimeline(unsigned long long* host_out) {
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
+  return CNMF_OK;
+}
 int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
   if (reset) {
@@ -3169,18 +3241,21 @@ static bool g_no_persist = getenv("CNMF_PERSIST") && strcmp(getenv("CNMF_PERSIST
 // prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2); CNMF_WRES=0 keeps W streaming
 static int g_persist_pd = (getenv("CNMF_PERSIST_PD") && atoi(getenv("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
 static bool g_no_wres = getenv("CNMF_WRES") && strcmp(getenv("CNMF_WRES"), "0") == 0;
-static PassFn persist_fn(bool wres = false) {
+static PassFn persist_fn(bool wres = false, bool multi = false) {
+  if (multi)  // the multi-GPU launch: PD = 2 only
+    return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true>)
+                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, false, true>);
   if (g_persist_pd == 1)
     return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, false>);
   return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, false>);
 }
 
-static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k) {
+static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k, bool multi = false) {
   if (g_no_persist || !use_sl(x_dtype, F, k) || n_rows % TS != 0) return 0;
   const int64_t n_tiles = n_rows / TS;
   const int min_tiles = g_persist_pd + 2;  // per workgroup (the W re-read hazard, see the kernel)
   if (n_tiles < min_tiles) return 0;
-  const int64_t maxb = max_resident(persist_fn(), sl::L_PTOTAL);
+  const int64_t maxb = max_resident(persist_fn(false, multi), sl::L_PTOTAL);
   if (maxb <= 0) return -1;
   int64_t n_full;
   bool tail;
@@ -3192,13 +3267,13 @@ static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k) {
 }
 
 // LDS of the W-resident variant for this grid, or 0 when it would lower the residency
-static size_t persist_wres_lds(int64_t n_rows, int64_t G) {
+static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
   if (g_no_wres || G <= 0) return 0;
   const int64_t nbt_max = (n_rows / TS + G - 1) / G;
   const size_t lds = (size_t)sl::L_PTOTAL + (size_t)nbt_max * sl::WB;
   if (lds > kMaxLds) return 0;
-  const int64_t base = max_resident(persist_fn(false), sl::L_PTOTAL);
-  const int64_t with = max_resident(persist_fn(true), lds);
+  const int64_t base = max_resident(persist_fn(false, multi), sl::L_PTOTAL);
+  const int64_t with = max_resident(persist_fn(true, multi), lds);
   return (with > 0 && with >= base) ? lds : 0;
 }
 
@@ -3210,11 +3285,64 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
 int64_t cnmf_counter_words(void) { return CNT_WORDS; }
 int cnmf_counter_err_word(void) { return CNT_ERR; }
 
+// ---- the multi-GPU exchange buffer (one per rank, IPC-shared): [2][world][K*V] fp64 slots, then
+// world flags at 64-byte strides.  Fine-grained device memory, so a peer's system-scope stores and
+// loads over xGMI are coherent with this GPU's while both kernels run.
+constexpr int XBUF_MAX_WORLD = 64;
+static size_t xbuf_flag_offset(int world) {
+  const size_t b = (size_t)2 * world * sl::K * sl::V * sizeof(double);
+  return (b + 255) & ~(size_t)255;
+}
+
+int64_t cnmf_xbuf_bytes(int world) {
+  if (world < 1 || world > XBUF_MAX_WORLD) return set_err(CNMF_ERR_ARG, "world must be in [1, %d]", XBUF_MAX_WORLD);
+  return (int64_t)(xbuf_flag_offset(world) + (size_t)64 * world);
+}
+
+int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle) {
+  if (!dptr || !ipc_handle) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  const int64_t bytes = cnmf_xbuf_bytes(world);
+  if (bytes < 0) return (int)bytes;
+  void* p = nullptr;
+  HIP_CHECK(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained));
+  hipError_t e = hipMemset(p, 0, (size_t)bytes);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(ipc_handle), p);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return set_err(CNMF_ERR_HIP, "exchange buffer: %s", hipGetErrorString(e));
+  }
+  *dptr = p;
+  return CNMF_OK;
+}
+
+int cnmf_xbuf_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+int cnmf_xbuf_open(const void* ipc_handle, void** dptr) {
+  if (!dptr || !ipc_handle) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  hipIpcMemHandle_t h;
+  memcpy(&h, ipc_handle, sizeof(h));
+  HIP_CHECK(hipIpcOpenMemHandle(dptr, h, hipIpcMemLazyEnablePeerAccess));
+  return CNMF_OK;
+}
+
+int cnmf_xbuf_close(void* dptr) {
+  HIP_CHECK(hipIpcCloseMemHandle(dptr));
+  return CNMF_OK;
+}
+
+int cnmf_xbuf_free(void* dptr) {
+  HIP_CHECK(hipFree(dptr));
+  return CNMF_OK;
+}
+
 // one cooperative launch of mu_iter_sl_kernel
 static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, double* H64, double* Ht,
                              double* HHt, double* partials, int64_t n_parts, double* stage,
                              uint32_t* counter, double* AB, int64_t n_rows, double l1_W, double l2_W,
-                             double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s) {
+                             double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s,
+                             double* const* peers = nullptr, int rank = 0, int world = 1,
+                             uint32_t gen0 = 0) {
   if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
                                   (long long)n_parts, (long long)G);
   PersistArgs pa;
@@ -3236,16 +3364,22 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.l2H = l2_H;
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
+  pa.peers = peers;
+  pa.rank = rank;
+  pa.world = world;
+  pa.gen0 = gen0;
+  pa.xflag_off = (int)xbuf_flag_offset(world);
+  const bool multi = peers != nullptr;
   void* args[] = {&pa};
-  const size_t wlds = n_iter > 1 ? persist_wres_lds(n_rows, G) : 0;
+  const size_t wlds = n_iter > 1 ? persist_wres_lds(n_rows, G, multi) : 0;
   // a plain launch: the grid is at most the occupancy query's co-resident capacity (persist_grid;
   // 106 SGPRs admit 6 workgroups per CU by MI355X_MICROARCH.md's residency formula, we use 2) and
   // every wait in the kernel is bounded, so a short residency ends in the error word, not a hang.
   // (hipLaunchCooperativeKernel made rocprofv3 crash at process exit and costs ~17 us per launch.)
   if (wlds)
-    HIP_CHECK(hipLaunchKernel(persist_fn(true), dim3((unsigned)G), dim3(NT), args, wlds, s));
+    HIP_CHECK(hipLaunchKernel(persist_fn(true, multi), dim3((unsigned)G), dim3(NT), args, wlds, s));
   else
-    HIP_CHECK(hipLaunchKernel(persist_fn(false), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, s));
+    HIP_CHECK(hipLaunchKernel(persist_fn(false, multi), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, s));
   return CNMF_OK;
 }
 
@@ -3284,6 +3418,11 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     pa.l2H = l2_H;
     pa.apply_first = apply_first;
     pa.apply_last = 0;
+    pa.peers = nullptr;
+    pa.rank = 0;
+    pa.world = 1;
+    pa.gen0 = 0;
+    pa.xflag_off = 0;
     void* args[] = {&pa};
     HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, hs));
     return CNMF_OK;
@@ -3334,6 +3473,34 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                             l2_H, stats, stream);
     if (st) return st;
   }
+  return CNMF_OK;
+}
+
+int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, double* H64,
+                             double* Ht, double* HHt, double* partials, int64_t n_parts,
+                             double* stage, uint32_t* counter, double* AB, int64_t n_rows,
+                             int n_features, int k, double l1_W, double l2_W, double l1_H,
+                             double l2_H, void* const* peers, int rank, int world, uint32_t gen0,
+                             void* const* events, int n_events, void* stream) {
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (n_iter <= 0) return CNMF_OK;
+  if (world < 1 || world > XBUF_MAX_WORLD || rank < 0 || rank >= world)
+    return set_err(CNMF_ERR_ARG, "rank %d / world %d out of range", rank, world);
+  if ((uint64_t)gen0 + (uint64_t)n_iter >= (uint64_t)sl::XPOISON)
+    return set_err(CNMF_ERR_ARG, "exchange generation overflow");
+  const int64_t G = persist_grid(n_rows, x_dtype, n_features, k, true);
+  if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (G == 0) return set_err(CNMF_ERR_UNSUPPORTED, "the in-launch multi-GPU path serves the persistent shape only");
+  if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !peers)
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+  int st = launch_persistent(G, n_iter, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB,
+                             n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs,
+                             reinterpret_cast<double* const*>(peers), rank, world, gen0);
+  if (st) return st;
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;
 }
 

@@ -13,9 +13,12 @@ all-reduces one double.  The sharding is exact: Σ_p W_pᵀX_p = WᵀX (tests/te
 """
 from __future__ import annotations
 
+import warnings
+
 import torch
 import torch.distributed as dist
 
+from . import _lib
 from .solver import MUPlan, run_mu
 
 __all__ = ["shard_bounds", "factorise_sharded"]
@@ -29,13 +32,19 @@ def shard_bounds(n_rows: int, world: int, rank: int):
 
 
 def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=0.0, l2_reg_W=0.0,
-                      l1_reg_H=0.0, l2_reg_H=0.0, update_H=True, group=None, device=None):
+                      l1_reg_H=0.0, l2_reg_H=0.0, update_H=True, group=None, device=None,
+                      exchange=False):
     """MU on this rank's rows; returns (W_shard, H, n_iter) as device tensors.
 
     X_shard: (n_r, F) float32/float64/bfloat16 tensor (any device; moved to `device`, default the
     current HIP device), W_shard: (n_r, k), H0: (k, F) identical on every rank (broadcast from rank 0
     here to make that true).  Regularisation constants are the already-scaled sklearn l1/l2 terms
     (SK:1254-1265 computed on the GLOBAL n_samples).
+
+    exchange=True: run each stretch of iterations as ONE persistent launch per rank with the
+    all-reduce inside the launch (peer exchange over xGMI, MUPlan.enable_exchange) when every
+    shard is a persistent shape (fp32, F = 81, k = 4, rows a multiple of 64); otherwise, or if the
+    buffers cannot be shared, a warning and the RCCL path.
     """
     if not (dist.is_available() and dist.is_initialized()):
         raise RuntimeError("factorise_sharded needs an initialised torch.distributed process group")
@@ -46,5 +55,11 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     plan = MUPlan(X, H0.shape[0], l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H, group=group)
     plan.set_W(torch.as_tensor(W_shard))
     plan.set_H(H0)
+    if exchange:
+        try:
+            plan.enable_exchange()
+        except _lib.HipLibraryError as e:
+            warnings.warn(f"in-launch exchange not used: {e}", RuntimeWarning)
     n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H)
+    plan.release()
     return plan.W, plan.H(), n_iter

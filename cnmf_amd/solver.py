@@ -86,9 +86,81 @@ class MUPlan:
         self.persistent_shape = bool(check(p, "cnmf_mu_persistent"))  # the persistent kernel serves it
         self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
+        self.exchange = False  # True: multi-GPU iterations as one launch per rank (enable_exchange)
         self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)
+
+    # -- multi-GPU with the all-reduce inside the launch ------------------------------------------
+    def enable_exchange(self):
+        """Set up the in-launch cross-rank all-reduce (cnmf_mu_iterations_multi): one fine-grained
+        exchange buffer per rank, IPC-shared with every peer (handles via all_gather_object on the
+        plan's group).  Collective: every rank of the group calls it.  Afterwards `iterate` runs
+        n iterations as ONE launch per rank.  Raises (on every rank) when any rank's shard is not a
+        persistent shape or any buffer cannot be shared; the plan then stays on the RCCL path."""
+        dist = torch.distributed
+        if self.group is None and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("enable_exchange needs an initialised torch.distributed group")
+        rank = dist.get_rank(self.group)
+        ok = torch.tensor([1.0 if self.persistent_shape else 0.0])
+        handle, ptr, err = None, ctypes.c_void_p(), ""
+        if self.persistent_shape:
+            hb = int(self.lib.cnmf_xbuf_handle_bytes())
+            hbuf = ctypes.create_string_buffer(hb)
+            with torch.cuda.device(self.device):
+                st = self.lib.cnmf_xbuf_alloc(self.world, ctypes.byref(ptr), hbuf)
+            if st < 0:
+                ok[0], err = 0.0, self.lib.cnmf_last_error().decode()
+            else:
+                handle = hbuf.raw
+        handles = [None] * self.world
+        dist.all_gather_object(handles, (rank, float(ok[0]), handle, err), group=self.group)
+        bad = [h for h in handles if h[1] == 0.0]
+        if bad:
+            if ptr.value:
+                self.lib.cnmf_xbuf_free(ptr)
+            raise _lib.HipLibraryError("in-launch exchange unavailable: " + "; ".join(
+                f"rank {r}: {e or 'shard is not a persistent shape'}" for r, _, _, e in bad))
+        opened, peers, err = [], [], ""
+        with torch.cuda.device(self.device):
+            for r, _, h, _ in sorted(handles, key=lambda x: x[0]):
+                if r == rank:
+                    peers.append(ptr.value)
+                    continue
+                q = ctypes.c_void_p()
+                if self.lib.cnmf_xbuf_open(h, ctypes.byref(q)) < 0:
+                    err = f"rank {rank} cannot open rank {r}'s buffer: " + self.lib.cnmf_last_error().decode()
+                    break
+                opened.append(q.value)
+                peers.append(q.value)
+        res = [None] * self.world
+        dist.all_gather_object(res, err, group=self.group)
+        if any(res):
+            for q in opened:
+                self.lib.cnmf_xbuf_close(ctypes.c_void_p(q))
+            self.lib.cnmf_xbuf_free(ptr)
+            raise _lib.HipLibraryError("in-launch exchange unavailable: " + "; ".join(e for e in res if e))
+        self._xbuf, self._xopened = ptr.value, opened
+        self.peers = torch.tensor(peers, dtype=torch.int64, device=self.device)
+        self.xrank, self.xgen = rank, 0
+        self.exchange = True
+        self.persistent = True
+        self.shard_steps = False
+
+    def disable_exchange(self):
+        """Back to shard steps + RCCL (the buffers stay mapped until the plan is released)."""
+        self.exchange = False
+        self.persistent = self.persistent_shape and self.world == 1
+
+    def release(self):
+        """Unmap / free the exchange buffers (not collective; the GPU must be idle)."""
+        if getattr(self, "_xbuf", None):
+            torch.cuda.synchronize(self.device)
+            for q in self._xopened:
+                self.lib.cnmf_xbuf_close(ctypes.c_void_p(q))
+            self.lib.cnmf_xbuf_free(ctypes.c_void_p(self._xbuf))
+            self._xbuf, self._xopened = None, []
+            self.exchange = False
 
     def use_shard_steps(self):
         """Run the multi-GPU iteration (one shard step + one all_reduce per iteration) even on a
@@ -151,7 +223,14 @@ class MUPlan:
         """Raise if a persistent launch gave up waiting for a workgroup (its results are invalid);
         synchronises the stream."""
         if getattr(self, "persistent", False) and int(self.counter[self.err_word].item()) != 0:
+            code = int(self.counter[self.err_word].item())
             self.counter[self.err_word] = 0
+            if getattr(self, "exchange", False):
+                self.disable_exchange()  # the buffer set's flags are poisoned: never reuse it
+                raise _lib.HipLibraryError(
+                    f"multi-GPU persistent launch failed (code {code}: 1 = a local workgroup, 2 = a "
+                    "peer rank timed out, 3 = a peer failed); the plan is back on the RCCL path and "
+                    "the results of that launch are invalid")
             raise _lib.HipLibraryError("persistent MU launch timed out waiting for a workgroup "
                                        "(grid not co-resident?); results of that launch are invalid")
 
@@ -164,6 +243,17 @@ class MUPlan:
         if not update_H:
             for _ in range(n_iter):  # transform: W only, H (and Ht/HHt) fixed (SK:854 skipped)
                 self.sample_pass(_lib.PASS_UPDATE_W)
+            return
+        if getattr(self, "exchange", False):
+            with torch.cuda.device(self.device):
+                check(self.lib.cnmf_mu_iterations_multi(
+                    n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
+                    _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
+                    _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.peers), self.xrank,
+                    self.world, self.xgen, *_event_array(pass_events), self._stream()),
+                    "cnmf_mu_iterations_multi")
+            self.xgen += n_iter
             return
         if self.world == 1 and not self.shard_steps:
             with torch.cuda.device(self.device):

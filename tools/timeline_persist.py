@@ -23,6 +23,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--exchange", action="store_true",
+                    help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
     a = ap.parse_args()
     import torch
     from cnmf_amd import _lib
@@ -38,6 +40,14 @@ def main():
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     assert plan.persistent
+    if a.exchange:
+        import socket
+        import torch.distributed as dist
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        plan.enable_exchange()
     plan.iterate(5)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -106,6 +116,21 @@ def main():
     summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
                     "us_per_iter": round(launch_us / a.iters, 2),
                     "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})
+    if a.exchange:
+        fx = lib.cnmf_debug_xtimeline
+        fx.argtypes = [ctypes.c_void_p]
+        fx.restype = ctypes.c_int
+        xb = np.zeros(TL_IT * 4, dtype=np.uint64)
+        _lib.check(fx(xb.ctypes.data), "xtimeline")
+        x = xb.reshape(TL_IT, 4).astype(np.int64)[1:n - 1]
+        p_ = pub[1:n - 1]
+        summary["exchange_us_median"] = {
+            "group_sum_to_start": None,
+            "slot_stores": round(float(np.median(x[:, 1] - x[:, 0])) * 10 / 1e3, 2),
+            "flag_wait": round(float(np.median(x[:, 2] - x[:, 1])) * 10 / 1e3, 2),
+            "slot_loads_sum": round(float(np.median(x[:, 3] - x[:, 2])) * 10 / 1e3, 2),
+            "to_publish": round(float(np.median(p_ - x[:, 3])) * 10 / 1e3, 2),
+            "arrival_to_start": round(float(np.median(x[:, 0] - arr[1:n - 1].max(axis=1))) * 10 / 1e3, 2)}
     print(json.dumps(summary), flush=True)
     for r in rows[:5]:
         print(json.dumps({k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}), flush=True)

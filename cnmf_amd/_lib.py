@@ -73,9 +73,11 @@ _SIGS = {
     "cnmf_xbuf_open": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "cnmf_xbuf_close": (_i32, [_vp]),
     "cnmf_xbuf_free": (_i32, [_vp]),
+    "cnmf_xctl_words": (_i64, [_i32]),
+    "cnmf_xctl_init": (_i32, [_vp, _vp, _i32, _i32]),
     "cnmf_mu_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
-                                        _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _i32,
-                                        ctypes.c_uint32, _vp, _i32, _vp]),
+                                        _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp, _i32,
+                                        _vp]),
 }
 
 

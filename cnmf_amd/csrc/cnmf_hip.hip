@@ -1934,14 +1934,16 @@ struct PersistArgs {
   double l1W, l2W, l1H, l2H;
   int apply_first;   // first apply the pending basis update from AB (multi-GPU: AB all-reduced)
   int apply_last;    // apply the last iteration's basis update in-launch (single GPU)
-  // MULTI (one persistent launch per rank, the all-reduce in-launch): every rank's exchange buffer
-  // (fine-grained, IPC-mapped): slots [world][K*V] doubles, then one flag per source rank at 64-B
-  // strides (xflag_off bytes in); flags carry gen0 + it + 1 (monotonic across launches)
-  double* const* peers;
-  int rank, world;
-  uint32_t gen0;
-  int xflag_off;
+  // MULTI (one persistent launch per rank, the all-reduce in-launch): the exchange control block
+  // (XC_* words, device memory), read only inside the exchange so that its values do not occupy
+  // SGPRs through the streaming loop
+  uint64_t* xctl;
 };
+
+// exchange control block words: rank, world, byte offset of the flags in an exchange buffer, the
+// generation base (advanced by n_iter at the end of every launch, on the device), then the
+// world exchange-buffer pointers (this rank's own at XC_PEERS + rank)
+constexpr int XC_RANK = 0, XC_WORLD = 1, XC_FLAG_OFF = 2, XC_GEN = 3, XC_PEERS = 8;
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2138,39 +2140,78 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) {
-          // ---- the cross-rank all-reduce of AB (k(F+k) fp64), inside the launch: this rank's AB
-          // into slot `rank` of every rank's exchange buffer (remote stores over xGMI, system
-          // scope), a system-scope release, one flag per destination; then wait for every rank's
-          // flag in this rank's buffer and sum the slots in rank order (the same AB, bit for bit,
-          // on every rank).  Slots alternate by generation parity: a rank writes generation g+2
-          // only after it has seen every rank's flag g+1, which each rank raises only after it
-          // has read its generation-g slots.  A rank whose launch has failed raises XPOISON
-          // instead, which makes every peer fail too (no rank waits out its timeout per iteration).
+          // ---- the cross-rank all-reduce of AB (k(F+k) fp64), inside the launch.  Each fp64
+          // value travels as two 64-bit words {generation tag : 32-bit half} (the LL protocol),
+          // written with system-scope atomic stores into slot `rank` of every rank's exchange
+          // buffer (remote stores over xGMI); a reader polls its own buffer until every word of
+          // every slot carries this generation's tag, so no separate flag, fence or store
+          // acknowledgement sits on the critical path.  Slots are summed in rank order: the same
+          // AB, bit for bit, on every rank.  Slots alternate by generation parity: rank p writes
+          // generation g+2 only after it has read every rank's g+1 words, which each rank writes
+          // only after it has read its generation-g slots.  A rank whose launch has failed tags
+          // its words XPOISON, which makes every peer fail too (no rank waits out its timeout per
+          // iteration).  The thread <-> element mapping is sum_rows_sc1's (o = t, t + NT).
           constexpr int n_out = K * V;
-          const uint32_t gen = a.gen0 + (uint32_t)it + 1u;
+          static_assert(n_out <= 2 * NT && n_out > NT, "two elements per thread");
+          // atomics: loaded here, not hoisted to the kernel entry
+          const int xrank = (int)__hip_atomic_load(a.xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int xworld = (int)__hip_atomic_load(a.xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint32_t gen =
+              (uint32_t)__hip_atomic_load(a.xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint32_t)it + 1u;
+          auto peer = [&](int r) {
+            return reinterpret_cast<uint64_t*>(
+                __hip_atomic_load(a.xctl + XC_PEERS + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          };
           TL_X(it, 0);
-          const size_t par = (size_t)(gen & 1u) * a.world * n_out;
-          for (int pr = 0; pr < a.world; ++pr) {
-            double* dst = a.peers[pr] + par + (size_t)a.rank * n_out;
-            for (int e = t; e < n_out; e += NT)
-              __hip_atomic_store(dst + e, sAB[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-          // every slot store is a system-scope atomic to fine-grained memory: once vmcnt(0) says
-          // it is acknowledged it is visible to every agent, so the flag can follow without a
-          // release fence (whose L2 writeback, buffer_wbl2, would stall this XCD for microseconds)
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __syncthreads();
-          TL_X(it, 1);
-          if (t < a.world) {
+          const bool has1 = t + NT < n_out;
+          const size_t slot = 2 * (size_t)n_out;  // words per rank slot
+          const size_t par = (size_t)(gen & 1u) * xworld * slot;
+          {
             const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-            uint32_t* f = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(a.peers[t]) +
-                                                      a.xflag_off + 64 * a.rank);
-            __hip_atomic_store(f, bad ? XPOISON : gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const uint32_t* mf = reinterpret_cast<const uint32_t*>(
-                reinterpret_cast<const unsigned char*>(a.peers[a.rank]) + a.xflag_off + 64 * t);
+            const uint64_t tag = (uint64_t)(bad ? XPOISON : gen) << 32;
+            const uint64_t b0 = (uint64_t)__double_as_longlong(sAB[t]);
+            const uint64_t b1 = has1 ? (uint64_t)__double_as_longlong(sAB[t + NT]) : 0ull;
+            for (int pr = 0; pr < xworld; ++pr) {
+              uint64_t* dst = peer(pr) + par + (size_t)xrank * slot;
+              __hip_atomic_store(dst + 2 * t, tag | (b0 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(dst + 2 * t + 1, tag | (b0 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              if (has1) {
+                __hip_atomic_store(dst + 2 * (t + NT), tag | (b1 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(dst + 2 * (t + NT) + 1, tag | (b1 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              }
+            }
+          }
+          TL_X(it, 1);
+          const uint64_t* mine = peer(xrank) + par;
+          double v0 = 0.0, v1 = 0.0;
+          constexpr int QB = 4;  // ranks polled per round (their loads in flight together)
+          for (int q0 = 0; q0 < xworld; q0 += QB) {
+            uint64_t w[QB][4];
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            uint32_t v;
-            while ((v = __hip_atomic_load(mf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) < gen) {
+            while (true) {
+#pragma unroll
+              for (int j = 0; j < QB; ++j) {
+                const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
+                w[j][0] = __hip_atomic_load(src + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                w[j][1] = __hip_atomic_load(src + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const int o1 = has1 ? t + NT : t;
+                w[j][2] = __hip_atomic_load(src + 2 * o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                w[j][3] = __hip_atomic_load(src + 2 * o1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              }
+              bool ok = true, poison = false;
+#pragma unroll
+              for (int j = 0; j < QB; ++j)
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                  const uint32_t tg = (uint32_t)(w[j][m] >> 32);
+                  ok = ok && tg == gen;
+                  poison = poison || tg == XPOISON;
+                }
+              if (ok) break;
+              if (poison) {
+                __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
               if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
               if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
                 __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2178,19 +2219,20 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
               }
               __builtin_amdgcn_s_sleep(1);
             }
-            if (v == XPOISON) __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int j = 0; j < QB; ++j) {
+              if (q0 + j < xworld) {  // rank order
+                v0 += __longlong_as_double((long long)((w[j][1] << 32) | (w[j][0] & 0xFFFFFFFFull)));
+                v1 += __longlong_as_double((long long)((w[j][3] << 32) | (w[j][2] & 0xFFFFFFFFull)));
+              }
+            }
           }
-          // no acquire fence either: the slot loads below are system-scope atomics (they bypass
-          // the caches) issued only after the flag value has come back
-          __syncthreads();
           TL_X(it, 2);
-          const double* mine = a.peers[a.rank] + par;
-          for (int e = t; e < n_out; e += NT) {
-            double v = 0.0;
-            for (int q = 0; q < a.world; ++q)
-              v += __hip_atomic_load(mine + (size_t)q * n_out + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            sAB[e] = v;
-            st_sc1(a.AB + e, v);
+          sAB[t] = v0;
+          st_sc1(a.AB + t, v0);
+          if (has1) {
+            sAB[t + NT] = v1;
+            st_sc1(a.AB + t + NT, v1);
           }
           TL_X(it, 3);
         }
@@ -2225,6 +2267,8 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
@@ -3285,18 +3329,17 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
 int64_t cnmf_counter_words(void) { return CNT_WORDS; }
 int cnmf_counter_err_word(void) { return CNT_ERR; }
 
-// ---- the multi-GPU exchange buffer (one per rank, IPC-shared): [2][world][K*V] fp64 slots, then
-// world flags at 64-byte strides.  Fine-grained device memory, so a peer's system-scope stores and
-// loads over xGMI are coherent with this GPU's while both kernels run.
+// ---- the multi-GPU exchange buffer (one per rank, IPC-shared): [2][world][2·K·V] tagged words
+// (see the MULTI block of mu_iter_sl_kernel).  Fine-grained device memory, so a peer's
+// system-scope stores and loads over xGMI are coherent with this GPU's while both kernels run.
 constexpr int XBUF_MAX_WORLD = 64;
-static size_t xbuf_flag_offset(int world) {
-  const size_t b = (size_t)2 * world * sl::K * sl::V * sizeof(double);
-  return (b + 255) & ~(size_t)255;
+static size_t xbuf_bytes(int world) {  // [2 parities][world][2·K·V] tagged 64-bit words
+  return (size_t)2 * world * 2 * sl::K * sl::V * sizeof(uint64_t);
 }
 
 int64_t cnmf_xbuf_bytes(int world) {
   if (world < 1 || world > XBUF_MAX_WORLD) return set_err(CNMF_ERR_ARG, "world must be in [1, %d]", XBUF_MAX_WORLD);
-  return (int64_t)(xbuf_flag_offset(world) + (size_t)64 * world);
+  return (int64_t)xbuf_bytes(world);
 }
 
 int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle) {
@@ -3341,8 +3384,7 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
                              double* HHt, double* partials, int64_t n_parts, double* stage,
                              uint32_t* counter, double* AB, int64_t n_rows, double l1_W, double l2_W,
                              double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s,
-                             double* const* peers = nullptr, int rank = 0, int world = 1,
-                             uint32_t gen0 = 0) {
+                             uint64_t* xctl = nullptr) {
   if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
                                   (long long)n_parts, (long long)G);
   PersistArgs pa;
@@ -3364,12 +3406,8 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.l2H = l2_H;
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
-  pa.peers = peers;
-  pa.rank = rank;
-  pa.world = world;
-  pa.gen0 = gen0;
-  pa.xflag_off = (int)xbuf_flag_offset(world);
-  const bool multi = peers != nullptr;
+  pa.xctl = xctl;
+  const bool multi = xctl != nullptr;
   void* args[] = {&pa};
   const size_t wlds = n_iter > 1 ? persist_wres_lds(n_rows, G, multi) : 0;
   // a plain launch: the grid is at most the occupancy query's co-resident capacity (persist_grid;
@@ -3418,11 +3456,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     pa.l2H = l2_H;
     pa.apply_first = apply_first;
     pa.apply_last = 0;
-    pa.peers = nullptr;
-    pa.rank = 0;
-    pa.world = 1;
-    pa.gen0 = 0;
-    pa.xflag_off = 0;
+    pa.xctl = nullptr;
     void* args[] = {&pa};
     HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, hs));
     return CNMF_OK;
@@ -3476,29 +3510,46 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
   return CNMF_OK;
 }
 
+int64_t cnmf_xctl_words(int world) {
+  if (world < 1 || world > XBUF_MAX_WORLD) return set_err(CNMF_ERR_ARG, "world must be in [1, %d]", XBUF_MAX_WORLD);
+  return XC_PEERS + world;
+}
+
+int cnmf_xctl_init(uint64_t* xctl, void* const* peers, int rank, int world) {
+  if (!xctl || !peers) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (world < 1 || world > XBUF_MAX_WORLD || rank < 0 || rank >= world)
+    return set_err(CNMF_ERR_ARG, "rank %d / world %d out of range", rank, world);
+  uint64_t h[XC_PEERS + XBUF_MAX_WORLD] = {0};
+  h[XC_RANK] = (uint64_t)rank;
+  h[XC_WORLD] = (uint64_t)world;
+  h[XC_FLAG_OFF] = 0;  // (unused: the words carry their own tags)
+  h[XC_GEN] = 0;
+  for (int r = 0; r < world; ++r) {
+    if (!peers[r]) return set_err(CNMF_ERR_ARG, "null exchange buffer of rank %d", r);
+    h[XC_PEERS + r] = reinterpret_cast<uint64_t>(peers[r]);
+  }
+  HIP_CHECK(hipMemcpy(xctl, h, sizeof(uint64_t) * (XC_PEERS + world), hipMemcpyHostToDevice));
+  return CNMF_OK;
+}
+
 int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, double* H64,
                              double* Ht, double* HHt, double* partials, int64_t n_parts,
                              double* stage, uint32_t* counter, double* AB, int64_t n_rows,
                              int n_features, int k, double l1_W, double l2_W, double l1_H,
-                             double l2_H, void* const* peers, int rank, int world, uint32_t gen0,
-                             void* const* events, int n_events, void* stream) {
+                             double l2_H, uint64_t* xctl, void* const* events, int n_events,
+                             void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   if (n_iter <= 0) return CNMF_OK;
-  if (world < 1 || world > XBUF_MAX_WORLD || rank < 0 || rank >= world)
-    return set_err(CNMF_ERR_ARG, "rank %d / world %d out of range", rank, world);
-  if ((uint64_t)gen0 + (uint64_t)n_iter >= (uint64_t)sl::XPOISON)
-    return set_err(CNMF_ERR_ARG, "exchange generation overflow");
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k, true);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G == 0) return set_err(CNMF_ERR_UNSUPPORTED, "the in-launch multi-GPU path serves the persistent shape only");
-  if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !peers)
+  if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   int st = launch_persistent(G, n_iter, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB,
-                             n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs,
-                             reinterpret_cast<double* const*>(peers), rank, world, gen0);
+                             n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs, xctl);
   if (st) return st;
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;

@@ -141,8 +141,12 @@ class MUPlan:
             self.lib.cnmf_xbuf_free(ptr)
             raise _lib.HipLibraryError("in-launch exchange unavailable: " + "; ".join(e for e in res if e))
         self._xbuf, self._xopened = ptr.value, opened
-        self.peers = torch.tensor(peers, dtype=torch.int64, device=self.device)
-        self.xrank, self.xgen = rank, 0
+        self.xctl = torch.zeros(int(check(self.lib.cnmf_xctl_words(self.world), "cnmf_xctl_words")),
+                                dtype=torch.int64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_xctl_init(_ptr(self.xctl), (ctypes.c_void_p * self.world)(*peers),
+                                          rank, self.world), "cnmf_xctl_init")
+        self.xrank = rank
         self.exchange = True
         self.persistent = True
         self.shard_steps = False
@@ -250,10 +254,8 @@ class MUPlan:
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
                     _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
-                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.peers), self.xrank,
-                    self.world, self.xgen, *_event_array(pass_events), self._stream()),
-                    "cnmf_mu_iterations_multi")
-            self.xgen += n_iter
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl),
+                    *_event_array(pass_events), self._stream()), "cnmf_mu_iterations_multi")
             return
         if self.world == 1 and not self.shard_steps:
             with torch.cuda.device(self.device):

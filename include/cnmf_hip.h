@@ -132,28 +132,32 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
 
 /* ---- Multi-GPU with the all-reduce inside the persistent launch (persistent shapes only).
  * Each rank allocates one exchange buffer (fine-grained device memory, zeroed) and exports its IPC
- * handle (cnmf_xbuf_handle_bytes() bytes); every rank opens every peer's handle, builds a device
- * array peers[world] of the buffer pointers (its own at peers[rank]) and then runs
- *   cnmf_mu_iterations_multi(n, ..., peers, rank, world, gen0, ...)
+ * handle (cnmf_xbuf_handle_bytes() bytes); every rank opens every peer's handle and writes the
+ * pointers (its own at [rank]) into a device control block of cnmf_xctl_words(world) uint64 words
+ * with cnmf_xctl_init; then
+ *   cnmf_mu_iterations_multi(n, ..., xctl, ...)
  * = n iterations of SK:831-870 over the union of the shards, as ONE launch per rank: each
  * iteration's [WᵀX | WᵀW] goes to every peer over xGMI and is summed in rank order (the same AB on
  * every rank, bit for bit); the last iteration's basis update is applied in-launch like
- * cnmf_mu_iterations.  gen0 = the total iterations this buffer set has run (the same on all ranks;
- * the exchange flags carry gen0 + it + 1).  Every wait is bounded: a rank that times out sets the
- * counter's error word and poisons its flags so that every peer's launch fails too; the buffer set
- * is then unusable (fall back to cnmf_mu_shard_step + an RCCL all-reduce). */
+ * cnmf_mu_iterations.  The control block also holds the exchange generation (word 3), advanced
+ * on the device by every launch, so all ranks must issue the same sequence of launches.  Every wait
+ * is bounded: a rank that times out sets the counter's error word and poisons its flags so that
+ * every peer's launch fails too; the buffer set is then unusable (fall back to
+ * cnmf_mu_shard_step + an RCCL all-reduce). */
 int64_t cnmf_xbuf_bytes(int world);
 int cnmf_xbuf_handle_bytes(void);
 int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle);
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr);
 int cnmf_xbuf_close(void* dptr);
 int cnmf_xbuf_free(void* dptr);
+int64_t cnmf_xctl_words(int world);
+int cnmf_xctl_init(uint64_t* xctl, void* const* peers, int rank, int world);
 int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, double* H64,
                              double* Ht, double* HHt, double* partials, int64_t n_parts,
                              double* stage, uint32_t* counter, double* AB, int64_t n_rows,
                              int n_features, int k, double l1_W, double l2_W, double l1_H,
-                             double l2_H, void* const* peers, int rank, int world, uint32_t gen0,
-                             void* const* events, int n_events, void* stream);
+                             double l2_H, uint64_t* xctl, void* const* events, int n_events,
+                             void* stream);
 
 /* Normalisation projection (no sklearn counterpart, off unless asked for):
  *   s_j = ‖H_j‖ (norm 1 = L1, 2 = L2, 3 = max; s_j := 1 for an all-zero row),

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=1000, help="iterations before the stamped launch (clock ramp)")
     ap.add_argument("--exchange", action="store_true",
                     help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
     a = ap.parse_args()
@@ -48,7 +49,7 @@ def main():
             port = so.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         plan.enable_exchange()
-    plan.iterate(5)
+    plan.iterate(a.warmup)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

@@ -69,6 +69,8 @@ _SIGS = {
                                   _i32, _f64, _f64, _f64, _f64, _i32, _vp]),
     "cnmf_xbuf_bytes": (_i64, [_i32]),
     "cnmf_xbuf_handle_bytes": (_i32, []),
+    "cnmf_device_pci_bus_id": (_i32, [_i32, ctypes.c_char_p, _i32]),
+    "cnmf_device_can_access_peer": (_i32, [_i32, _i32]),
     "cnmf_xbuf_alloc": (_i32, [_i32, ctypes.POINTER(_vp), _vp]),
     "cnmf_xbuf_open": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "cnmf_xbuf_close": (_i32, [_vp]),

@@ -3361,6 +3361,18 @@ int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle) {
 
 int cnmf_xbuf_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
 
+int cnmf_device_pci_bus_id(int device, char* out, int len) {
+  if (!out || len < 16) return set_err(CNMF_ERR_ARG, "buffer too small");
+  HIP_CHECK(hipDeviceGetPCIBusId(out, len, device));
+  return CNMF_OK;
+}
+
+int cnmf_device_can_access_peer(int device, int peer) {
+  int ok = 0;
+  HIP_CHECK(hipDeviceCanAccessPeer(&ok, device, peer));
+  return ok ? 1 : 0;
+}
+
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr) {
   if (!dptr || !ipc_handle) return set_err(CNMF_ERR_ARG, "null pointer argument");
   hipIpcMemHandle_t h;

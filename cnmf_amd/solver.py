@@ -104,7 +104,16 @@ class MUPlan:
         rank = dist.get_rank(self.group)
         ok = torch.tensor([1.0 if self.persistent_shape else 0.0])
         handle, ptr, err = None, ctypes.c_void_p(), ""
-        if self.persistent_shape:
+        # peer reachability first: every peer's GPU that this process can see must be mappable
+        devs = [None] * self.world
+        dist.all_gather_object(devs, (rank, self._pci_bus_id(self.device.index)), group=self.group)
+        local = {self._pci_bus_id(j): j for j in range(torch.cuda.device_count())}
+        for r, bus in devs:
+            j = local.get(bus)
+            if r != rank and j is not None and j != self.device.index and \
+                    self.lib.cnmf_device_can_access_peer(self.device.index, j) != 1:
+                ok[0], err = 0.0, f"no peer access from device {self.device.index} to {j} ({bus})"
+        if self.persistent_shape and ok[0] != 0.0:
             hb = int(self.lib.cnmf_xbuf_handle_bytes())
             hbuf = ctypes.create_string_buffer(hb)
             with torch.cuda.device(self.device):
@@ -150,6 +159,11 @@ class MUPlan:
         self.exchange = True
         self.persistent = True
         self.shard_steps = False
+
+    def _pci_bus_id(self, dev: int) -> str:
+        buf = ctypes.create_string_buffer(64)
+        check(self.lib.cnmf_device_pci_bus_id(dev, buf, 64), "cnmf_device_pci_bus_id")
+        return buf.value.decode().lower()
 
     def disable_exchange(self):
         """Back to shard steps + RCCL (the buffers stay mapped until the plan is released)."""

@@ -146,6 +146,10 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
  * cnmf_mu_shard_step + an RCCL all-reduce). */
 int64_t cnmf_xbuf_bytes(int world);
 int cnmf_xbuf_handle_bytes(void);
+/* Peer checks before the exchange: the PCI bus id of a visible device ("dddd:bb:dd.f", len >= 16)
+ * and whether `device` can map `peer`'s memory (1 / 0). */
+int cnmf_device_pci_bus_id(int device, char* out, int len);
+int cnmf_device_can_access_peer(int device, int peer);
 int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle);
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr);
 int cnmf_xbuf_close(void* dptr);

@@ -60,6 +60,8 @@ def parse():
                    help="multi-GPU MU: auto = the all-reduce inside the persistent launch (peer "
                         "exchange over xGMI), validated against the RCCL path before timing and "
                         "replaced by it on any failure; off = shard step + RCCL all_reduce")
+    p.add_argument("--no-tune", action="store_true",
+                   help="skip timing the two persistent-launch layouts (MUPlan.tune) before the run")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
@@ -249,6 +251,15 @@ def main():
             plan.iterate(args.warmup)
             torch.cuda.synchronize()
 
+    # the persistent launch has two layouts whose order differs between boxes: time both on this
+    # box (warm clocks; copies of W / H, so the state is unchanged) and keep the faster
+    tuned = {}
+    if args.solver == "mu" and plan.persistent and not args.no_tune:
+        tuned = plan.tune(n_iter=100, rounds=2)
+        print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
+    layout = {1: "pairs of 4-wave workgroups per CU", 2: "one 8-wave two-team workgroup per CU"}.get(
+        int(plan.lib.cnmf_get_persist_variant())) if plan.persistent else None
+
     K = args.steps
 
     def timed():
@@ -382,7 +393,9 @@ def main():
                    "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64"
                                   + (", in-launch over xGMI)" if plan.exchange else ", RCCL)")
                                   + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
-                   "exchange": exchange},
+                   "exchange": exchange,
+                   "persistent_layout": layout,
+                   "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

@@ -58,6 +58,8 @@ _SIGS = {
     "cnmf_mu_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                   _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _vp]),
     "cnmf_counter_words": (_i64, []),
+    "cnmf_set_persist_variant": (_i32, [_i32]),
+    "cnmf_get_persist_variant": (_i32, []),
     "cnmf_counter_err_word": (_i32, []),
     "cnmf_mu_persistent": (_i32, [_i64, _i32, _i32, _i32]),
     "cnmf_als_table_doubles": (_i32, []),

@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <unordered_map>
@@ -1195,7 +1196,8 @@ __device__ __forceinline__ void phase1(unsigned char* smem, float (&xv)[NC], int
 // wres (W resident in LDS, mu_iter_sl_kernel<…, true>): this tile's W [64][4] is read from and
 // the new W written back to LDS; otherwise the staged tile is read and the new W stored to HBM.
 __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ W, int64_t tile, int wpar,
-                                       int wave, int lane, double l1, double l2, float* wres = nullptr) {
+                                       int wave, int lane, double l1, double l2, float* wres = nullptr,
+                                       bool active = true) {
   const double* sP = reinterpret_cast<const double*>(smem + L_P);
   const double* sHHt = reinterpret_cast<const double*>(smem + L_HHT);
   float* sWn = reinterpret_cast<float*>(smem + L_WN);
@@ -1216,11 +1218,15 @@ __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ 
   if (l2 > 0.0) den = den + l2 * wold;  // SK:618-619
   if (den == 0.0) den = EPS32;          // SK:620
   const float wn = (float)(wold * (num / den));  // SK:622-629
-  if (wres)
-    wres[s * K + j] = wn;  // the quad's float4 read above precedes this store (data dependence)
-  else
-    W[((size_t)tile * TS + s) * K + j] = wn;
-  sWn[s * K + j] = wn;
+  // inactive: a padding step of the team with one tile fewer (mu_iter_sl_kernel<…, 2>): nothing
+  // is stored and w' = 0 makes phase 3 add nothing
+  if (active) {
+    if (wres)
+      wres[s * K + j] = wn;  // the quad's float4 read above precedes this store (data dependence)
+    else
+      W[((size_t)tile * TS + s) * K + j] = wn;
+  }
+  sWn[s * K + j] = active ? wn : 0.f;
 }
 
 // phase 3: lane = sample; acc += w'ᵀ·[x | w'] on the registers of phase 1 (SK:639-640)
@@ -1246,9 +1252,13 @@ __device__ __forceinline__ void phase3(const unsigned char* smem, float (&xv)[NC
 // The workgroup's accumulators -> its fp64 partial row [K][V]: a DPP tree over each 16-lane row,
 // the 4 row sums of each wave through LDS (`red`, NWAVE*4*NR floats), the 4 waves summed in fp64.
 // SC1: store the row write-through (an in-launch hand-off, MI355X_MICROARCH.md valid-forms table).
-template <bool SC1>
+// TEAMS = 2 (the two 4-wave teams of an 8-wave workgroup, mu_iter_sl_kernel<…, 2>): each team
+// reduces into its own scratch `red`; after the barrier the 512 threads (tid) combine team 0's and
+// team 1's (`red0`, `red1`) wave sums in a fixed order into the workgroup's one row.
+template <bool SC1, int TEAMS = 1>
 __device__ __forceinline__ void flush_acc(float* red, float (&acc)[NC][K], float& acc33, double* prow,
-                                          int wave, int lane, int t) {
+                                          int wave, int lane, int t, const float* red0 = nullptr,
+                                          const float* red1 = nullptr, int tid = 0) {
   float* myred = red + (wave * 4 + (lane >> 4)) * NR;
 #pragma unroll
   for (int c = 0; c < NC; ++c)
@@ -1270,15 +1280,19 @@ __device__ __forceinline__ void flush_acc(float* red, float (&acc)[NC][K], float
     if ((lane & 15) == 0) myred[NC * K] = r;
   }
   lds_barrier();
-  for (int e = t; e < K * V; e += NT) {
+  for (int e = TEAMS == 1 ? t : tid; e < K * V; e += NT * TEAMS) {
     const int j = e / V;
     const int v = e - j * V;
     const int w = v < 3 * NF ? v / NF : 3;
     int idx;  // position inside wave w's row sums
     if (v < V - 1) idx = (v - NF * w) * K + j;
     else idx = j < K - 1 ? (NC - 3 + j) * K + (K - 1) : NC * K;  // column 84 = B[.][3] = B[3][.]
-    const float* rr = red + (w * 4) * NR + idx;
-    const double val = ((double)rr[0] + (double)rr[NR]) + ((double)rr[2 * NR] + (double)rr[3 * NR]);
+    const float* rr = (TEAMS == 1 ? red : red0) + (w * 4) * NR + idx;
+    double val = ((double)rr[0] + (double)rr[NR]) + ((double)rr[2 * NR] + (double)rr[3 * NR]);
+    if (TEAMS == 2) {
+      const float* r1 = red1 + (w * 4) * NR + idx;
+      val += ((double)r1[0] + (double)r1[NR]) + ((double)r1[2 * NR] + (double)r1[3 * NR]);
+    }
     if (SC1)
       __hip_atomic_store(prow + e, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else
@@ -2023,11 +2037,27 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
 // WRES: W stays resident in LDS for the whole launch (this workgroup's tiles, loaded once at the
 // start and written back once at the end): the passes stream only X, 324 instead of 356 bytes per
 // sample ("keep tensors resident instead of re-reading them").  Needs nbt·1 KB of extra LDS.
-template <int PD, bool WRES, bool MULTI = false>
-__global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(PersistArgs a) {
+//
+// TEAMS = 2: one 8-wave workgroup per CU made of two 4-wave teams, each running the tile pipeline
+// below on its own tiles and its own copy of the LDS layout (team 1's at smem + team_lds), in
+// lockstep: every barrier is the workgroup's.  Two independent 4-wave workgroups on a CU drift
+// apart (one of the pair finishes several microseconds after the other, and the iteration waits
+// for the slowest); in lockstep the pair shares the CU evenly.  The teams own virtual blocks
+// vb = 2b + team (tiles vb + 2G·i); the team with one tile fewer runs a padding step (nothing
+// stored, nothing accumulated) so both execute the same barriers.  The two teams' accumulators
+// are combined into the workgroup's one fp64 row in a fixed order (deterministic).
+#ifndef CNMF_TEAM_PRIO
+#define CNMF_TEAM_PRIO 1
+#endif
+constexpr bool SETPRIO = CNMF_TEAM_PRIO != 0;
+template <int PD, bool WRES, bool MULTI = false, int TEAMS = 1>
+__global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) void mu_iter_sl_kernel(PersistArgs a) {
   using namespace sl;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int t = threadIdx.x;
+  static_assert(TEAMS == 1 || (TEAMS == 2 && PD == 2), "two teams: PD = 2");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
+  const int tid = threadIdx.x;
+  const int team = TEAMS == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int t = TEAMS == 1 ? tid : (tid & (NT - 1));
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int b = blockIdx.x;
@@ -2037,9 +2067,19 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
   const int gs = (G - g + NG - 1) / NG;
   const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
   const unsigned char* Wb = reinterpret_cast<const unsigned char*>(a.W);
+  // tiles of this team: vb + Gv·i, i < nbt_team; the loop runs nbt (team 0's count) steps per
+  // iteration, the same every iteration.  The host guarantees nbt_team >= PD + 2, so a tile's W was
+  // stored at least one tile before it is prefetched again.
+  const int Gv = G * TEAMS;
+  const int vb = b * TEAMS + team;
+  const int nbt = (int)((a.n_tiles - (int64_t)b * TEAMS + Gv - 1) / Gv);
+  const int nbt_team = TEAMS == 1 ? nbt : (int)((a.n_tiles - vb + Gv - 1) / Gv);
+  const int nbt_max = (int)((a.n_tiles + Gv - 1) / Gv);
+  const int team_lds = L_PTOTAL + (WRES ? nbt_max * WB : 0);  // the host sizes TEAMS x this
+  unsigned char* smem = smem_base + (TEAMS == 1 ? 0 : team * team_lds);
   double* sH = reinterpret_cast<double*>(smem + L_H);
   double* sAB = reinterpret_cast<double*>(smem + L_AB);
-  int* sFlag = reinterpret_cast<int*>(smem + L_FLAG);
+  int* sFlag = reinterpret_cast<int*>(smem_base + L_FLAG);  // the workgroup's (team 0's copy)
   uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
   uint32_t* cnt_top = a.cnt + CNT_TOP;
   uint32_t* flag = a.cnt + CNT_FLAG;
@@ -2063,17 +2103,17 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     for (int j = 0; j < K; ++j) acc[c][j] = 0.f;
   float acc33 = 0.f;
 
-  // tiles of this workgroup: b + G·i, i < nbt, the same every iteration.  The host guarantees
-  // nbt >= PD + 2, so a tile's W was stored at least one tile before it is prefetched again.
-  const int nbt = (int)((a.n_tiles - b + G - 1) / G);
   const int total = a.n_iter * nbt;
-  auto tile_at = [&](int q) -> int64_t { return b + (int64_t)G * (q % nbt); };
+  auto tile_at = [&](int q) -> int64_t {
+    const int i = q % nbt;
+    return vb + (int64_t)Gv * (TEAMS == 1 ? i : min(i, nbt_team - 1));  // padding step: a valid tile
+  };
   unsigned char* wres = smem + L_PTOTAL;  // [nbt][64][4] fp32 when WRES
   if (WRES) {
-    for (int c = t; c < nbt * (WB / 16); c += NT) {
+    for (int c = t; c < nbt_team * (WB / 16); c += NT) {
       const int i = c / (WB / 16), ch = c - i * (WB / 16);
       *reinterpret_cast<u32x4*>(wres + i * WB + 16 * ch) =
-          *reinterpret_cast<const u32x4*>(Wb + (size_t)(b + (int64_t)G * i) * WB + 16 * ch);
+          *reinterpret_cast<const u32x4*>(Wb + (size_t)(vb + (int64_t)Gv * i) * WB + 16 * ch);
     }
   }
   u32x4 pfA[PFN], pfB[PFN];
@@ -2083,6 +2123,10 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
   if (total > PD) sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
   lds_barrier();
   TL_START;
+  // the second-dispatched half (waves 4-7) loses every VALU arbitration to its older SIMD partner
+  // at equal priority: one static raise, no per-segment flips (MI355X_MICROARCH.md, two waves per
+  // SIMD, item 4)
+  if (TEAMS == 2 && SETPRIO && team == 1) __builtin_amdgcn_s_setprio(1);
 
   bool alive = true;
   int wpar = 0;
@@ -2095,23 +2139,29 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     const bool hasP = q + 1 + PD < total;
     const int64_t tile = tile_at(q);
     float xv[NC];
+    // two teams run half a tile apart: team 1 passes one barrier before its first tile of the
+    // iteration and team 0 one after its last, so team 1's phase 1 overlaps team 0's phase 2 and
+    // staging (and vice versa) instead of both teams hitting the same resources at once
+    if (TEAMS == 2 && team == 1 && i == 0) lds_barrier();
     phase1(smem, xv, wave, lane);
     // this wave's W store of the previous tile has landed (vmcnt retires in order; at most the 6
     // loads issued after it may remain) before any wave passes barrier A and prefetches W again
     if (!WRES) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     lds_barrier();  // A
     phase2(smem, a.W, tile, wpar, wave, lane, a.l1W, a.l2W,
-           WRES ? reinterpret_cast<float*>(wres + i * WB) : nullptr);
+           WRES ? reinterpret_cast<float*>(wres + i * WB) : nullptr, TEAMS == 1 || i < nbt_team);
     if (has1) sl_stage<!WRES>(smem, wpar ^ 1, pf, t);
     if (hasP && !end_it) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);
     lds_barrier();  // B
     phase3(smem, xv, acc, acc33, wave, lane);
     wpar ^= 1;
     if (!end_it) return;
+    if (TEAMS == 2 && team == 0) lds_barrier();  // team 1's last tile
 
     // ---- end of the iteration: publish this workgroup's row, then the in-launch reduction
-    flush_acc<true>(reinterpret_cast<float*>(smem + L_RED), acc, acc33, a.partials + (size_t)b * (K * V),
-                    wave, lane, t);
+    flush_acc<true, TEAMS>(reinterpret_cast<float*>(smem + L_RED), acc, acc33, a.partials + (size_t)b * (K * V),
+                           wave, lane, t, reinterpret_cast<const float*>(smem_base + L_RED),
+                           reinterpret_cast<const float*>(smem_base + team_lds + L_RED), tid);
 #pragma unroll
     for (int c = 0; c < NC; ++c)
 #pragma unroll
@@ -2121,7 +2171,7 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     __syncthreads();
     if (hasP) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);  // in flight during the reduction
     TL(it, 0);
-    if (t == 0) {
+    if (tid == 0) {
       const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
       sFlag[1] = 0;
@@ -2129,15 +2179,15 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
     }
     __syncthreads();
     if (sFlag[0]) {  // group combiner
-      sum_rows_sc1(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * (K * V), t);
+      if (team == 0) sum_rows_sc1(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * (K * V), t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (t == 0) {
+      if (tid == 0) {
         const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
       }
       __syncthreads();
-      if (sFlag[1]) {  // top combiner: AB
+      if (sFlag[1] && team == 0) {  // top combiner: AB (team 0; team 1 copies it below)
         sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) {
           // ---- the cross-rank all-reduce of AB (k(F+k) fp64), inside the launch.  Each fp64
@@ -2236,26 +2286,34 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
           }
           TL_X(it, 3);
         }
+      }
+      if (sFlag[1]) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0 && !last_it)
+        if (tid == 0 && !last_it)
           __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         TL_PUB(it);
+        if (TEAMS == 2) {  // team 1's copy of AB
+          if (team == 1)
+            for (int e = t; e < K * V; e += NT) sAB[e] = reinterpret_cast<const double*>(smem_base + L_AB)[e];
+          __syncthreads();
+        }
       }
     }
     const bool top = sFlag[1] != 0;
     if (last_it) {
       alive = false;
-      if (WRES) {  // this workgroup's W back to HBM, once per launch
-        for (int c = t; c < nbt * (WB / 16); c += NT) {
+      if (WRES) {  // this team's W back to HBM, once per launch
+        for (int c = t; c < nbt_team * (WB / 16); c += NT) {
           const int ii = c / (WB / 16), ch = c - ii * (WB / 16);
-          *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(b + (int64_t)G * ii) * WB + 16 * ch) =
+          *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(vb + (int64_t)Gv * ii) * WB + 16 * ch) =
               *reinterpret_cast<const u32x4*>(wres + ii * WB + 16 * ch);
         }
       }
       if (!top) return;
       // the last combiner of the launch: every other workgroup has arrived for the last time
       if (a.apply_last) sl_update_basis(smem, t, a.l1H, a.l2H);
+      if (team != 0) return;
       for (int e = t; e < K * F; e += NT) a.H64[e] = sH[e];
       for (int e = t; e < F * K; e += NT) {
         const int f = e / K;
@@ -2264,7 +2322,7 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
       }
       if (t < K * K) a.HHt[t] = reinterpret_cast<const double*>(smem + L_HHT)[t];
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == 0) {
+      if (tid == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (MULTI)  // the next launch's generations follow this one's
@@ -2273,7 +2331,7 @@ __global__ __launch_bounds__(NT, PD == 1 ? 3 : 2) void mu_iter_sl_kernel(Persist
       return;
     }
     if (!top) {
-      if (t == 0) {
+      if (tid == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
@@ -3321,6 +3379,46 @@ static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
   return (with > 0 && with >= base) ? lds : 0;
 }
 
+// ---- the two-team variant (mu_iter_sl_kernel<2, true, MULTI, 2>: one 8-wave workgroup per CU, W
+// resident): multi-iteration launches of a shape whose W tiles fit in LDS twice over.  Which of the
+// two layouts is faster differs between boxes (same-box A/B, 500-iteration launches: 64.4 vs
+// 66.5 µs on one, 70.2 vs 67.3 µs on another), so it is a process-wide switch the host can set
+// after timing both (MUPlan.tune): 1 = pairs of 4-wave workgroups (the default), 2 = two teams.
+// CNMF_TEAMS=1|2 sets the initial value.
+static std::atomic<int> g_persist_variant{
+    (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 1};
+
+int cnmf_set_persist_variant(int v) {
+  if (v != 1 && v != 2) return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs) or 2 (teams)");
+  g_persist_variant.store(v);
+  return CNMF_OK;
+}
+int cnmf_get_persist_variant(void) { return g_persist_variant.load(); }
+static PassFn persist_teams_fn(bool multi) {
+  return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
+               : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 2>);
+}
+
+// workgroups (0: not eligible) and LDS bytes of a two-team launch over n_tiles (persist_grid > 0)
+static int64_t persist_teams_grid(int64_t n_tiles, bool multi, size_t* lds_out) {
+  if (g_persist_variant.load() != 2 || g_no_wres || g_persist_pd != 2) return 0;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (2 * (2 + 2)), (int64_t)sl::GROUP * sl::MAX_GROUPS});
+  if (G < 1) return 0;
+  const int64_t nbt_max = (n_tiles + 2 * G - 1) / (2 * G);
+  const size_t lds = 2 * ((size_t)sl::L_PTOTAL + (size_t)nbt_max * sl::WB);
+  if (lds > kMaxLds) return 0;
+  const PassFn fn = persist_teams_fn(multi);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 2 * NT, lds) != hipSuccess) return 0;
+  if (per_cu < 1) return 0;  // the whole grid must be co-resident: one workgroup per CU
+  *lds_out = lds;
+  return G;
+}
+
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
@@ -3421,6 +3519,15 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.xctl = xctl;
   const bool multi = xctl != nullptr;
   void* args[] = {&pa};
+  if (n_iter > 1) {
+    size_t tlds = 0;
+    const int64_t GT = persist_teams_grid(n_rows / TS, multi, &tlds);
+    if (GT > 0 && GT <= n_parts) {
+      pa.n_groups = (int)((GT + sl::GROUP - 1) / sl::GROUP);
+      HIP_CHECK(hipLaunchKernel(persist_teams_fn(multi), dim3((unsigned)GT), dim3(2 * NT), args, tlds, s));
+      return CNMF_OK;
+    }
+  }
   const size_t wlds = n_iter > 1 ? persist_wres_lds(n_rows, G, multi) : 0;
   // a plain launch: the grid is at most the occupancy query's co-resident capacity (persist_grid;
   // 106 SGPRs admit 6 workgroups per CU by MI355X_MICROARCH.md's residency formula, we use 2) and

@@ -293,6 +293,36 @@ class MUPlan:
             self._allreduce(self.AB)
         self.basis_update()
 
+    def tune(self, n_iter: int = 100, rounds: int = 2) -> dict:
+        """Time both layouts of the persistent launch (cnmf_set_persist_variant: 1 = pairs of
+        4-wave workgroups, 2 = 8-wave two-team workgroups) on this plan's shape and keep the faster
+        one for the process.  Runs on copies of W and H: the plan's state is unchanged.  Call after
+        the GPU has been busy for a while (the clock ramps up over the first ~35 ms of work).
+        Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent plans."""
+        if not self.persistent:
+            return {}
+        W0, H0 = self.W.clone(), self.H64.clone()
+        stream = torch.cuda.current_stream(self.device)
+        times = {1: [], 2: []}
+        try:
+            for _ in range(rounds):
+                for v in (1, 2):
+                    check(self.lib.cnmf_set_persist_variant(v), "cnmf_set_persist_variant")
+                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                    ev[0].record(stream)
+                    self.iterate(n_iter)
+                    ev[1].record(stream)
+                    torch.cuda.synchronize(self.device)
+                    self.check_sync_error()
+                    times[v].append(ev[0].elapsed_time(ev[1]) * 1e3 / n_iter)
+        finally:
+            self.W.copy_(W0)
+            self.H64.copy_(H0)
+            self.refresh_basis()
+        best = min(times, key=lambda v: sum(times[v]))
+        check(self.lib.cnmf_set_persist_variant(best), "cnmf_set_persist_variant")
+        return {v: sum(t) / len(t) for v, t in times.items()}
+
     _NORMS = {"l1": 1, "l2": 2, "max": 3}
 
     def normalise(self, norm: str = "l2") -> torch.Tensor:

@@ -105,6 +105,13 @@ int cnmf_counter_err_word(void);
  * iteration. */
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
 
+/* Process-wide layout of multi-iteration persistent launches (results agree to fp32 rounding of
+ * the per-workgroup partial sums, not bit for bit): 1 = two independent 4-wave workgroups per CU
+ * (default), 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart.
+ * The faster one differs between boxes; MUPlan.tune() times both and sets it. */
+int cnmf_set_persist_variant(int variant);
+int cnmf_get_persist_variant(void);
+
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
  * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction
  * and the basis update in-launch (stage then holds the group rows, counter: cnmf_counter_words()).

@@ -35,26 +35,68 @@ def _unfused(plan, n):
         plan.basis_update()
 
 
-@pytest.mark.parametrize("n_tiles", [40, 1000, 4096])
-def test_persistent_matches_oracle(n_tiles):
+@pytest.fixture(params=[1, 2], ids=["pairs", "teams"])
+def layout(request):
+    """The persistent launch's two layouts (cnmf_set_persist_variant): pairs of 4-wave workgroups
+    per CU, or one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart)."""
+    from cnmf_amd import _lib
+    lib = _lib.load()
+    old = lib.cnmf_get_persist_variant()
+    assert lib.cnmf_set_persist_variant(request.param) == 0
+    yield request.param
+    lib.cnmf_set_persist_variant(old)
+
+
+# 40 / 1000 / 4096 tiles: few tiles per (virtual) workgroup, a padding step for one of the teams
+# (odd per-workgroup tile counts), many groups; 15625 = cfg2's tile count
+@pytest.mark.parametrize("n_tiles", [40, 1000, 4095, 15625])
+def test_persistent_matches_oracle(n_tiles, layout):
     from cnmf_amd.synthetic import iop_spectra, random_init
     N = 64 * n_tiles
     X = iop_spectra(N, 81, seed=n_tiles, dtype=np.float32)
     W0, H0 = random_init(X, 4, 42)
     plan = _plan(X, W0, H0)
     assert plan.persistent, "shape should take the persistent launch"
-    plan.iterate(200)
+    n_it = 200 if n_tiles < 15625 else 40  # the full cfg2 size: a shorter oracle run
+    plan.iterate(n_it)
     plan.check_sync_error()
     W = plan.W.cpu().numpy()
     H = plan.H64.cpu().numpy()
     Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
-                              max_iter=200, tol=0.0)
+                              max_iter=n_it, tol=0.0)
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
     # Ht / HHt left behind for the loss pass and the next call are those of the final H
     Ht = plan.Ht.cpu().numpy()
     np.testing.assert_array_equal(Ht[:, :4], H.T)
     np.testing.assert_allclose(plan.HHt.cpu().numpy(), H @ H.T, rtol=1e-12)
     assert int(plan.counter.cpu().numpy().astype(np.int64).sum()) == 0  # counters back at rest
+
+
+def test_layouts_agree_and_are_deterministic():
+    """The two layouts group the per-workgroup fp32 partial sums differently: agreement to fp32
+    summation-order noise; each is bit-for-bit repeatable, also across split launches."""
+    import torch
+    from cnmf_amd import _lib
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    lib = _lib.load()
+    old = lib.cnmf_get_persist_variant()
+    X = iop_spectra(64 * 3001, 81, seed=21, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 5)
+    out = {}
+    try:
+        for v in (1, 2):
+            lib.cnmf_set_persist_variant(v)
+            a, c = _plan(X, W0, H0), _plan(X, W0, H0)
+            a.iterate(60)
+            for n in (7, 23, 30):
+                c.iterate(n)
+            a.check_sync_error()
+            c.check_sync_error()
+            assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
+            out[v] = (a.W.cpu().numpy(), a.H64.cpu().numpy())
+    finally:
+        lib.cnmf_set_persist_variant(old)
+    assert rel_fro(out[1][0], out[2][0]) < 1e-6 and rel_fro(out[1][1], out[2][1]) < 1e-6
 
 
 def test_persistent_agrees_with_per_iteration_launches():

@@ -373,7 +373,9 @@ def main():
                     f"{args.dtype} synthetic IOP spectra")
     else:
         metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
-        workload = (f"cfg2: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+        cfg = {(1_000_000, 81, 4, "f32"): "cfg2", (1_250_000, 81, 8, "f32"): "cfg3 (one GPU's shard)",
+               (1_000_000, 300, 16, "bf16"): "cfg4"}.get((n_rows, F, k, args.dtype), "custom")
+        workload = (f"{cfg}: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
                     f"{args.dtype} synthetic IOP spectra; rows sharded across GPUs")
     out = {
         "metric": metric,

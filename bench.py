@@ -61,7 +61,7 @@ def parse():
                         "exchange over xGMI), validated against the RCCL path before timing and "
                         "replaced by it on any failure; off = shard step + RCCL all_reduce")
     p.add_argument("--no-tune", action="store_true",
-                   help="skip timing the two persistent-launch layouts (MUPlan.tune) before the run")
+                   help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
@@ -257,7 +257,9 @@ def main():
     if args.solver == "mu" and plan.persistent and not args.no_tune:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
-    layout = {1: "pairs of 4-wave workgroups per CU", 2: "one 8-wave two-team workgroup per CU"}.get(
+    layout = {1: "pairs of 4-wave workgroups per CU", 2: "one 8-wave two-team workgroup per CU",
+              3: "pairs of 4-wave workgroups per CU with floating tiles (80 % resident, 20 % drawn "
+                 "from a pool every iteration)"}.get(
         int(plan.lib.cnmf_get_persist_variant())) if plan.persistent else None
 
     K = args.steps

@@ -60,6 +60,7 @@ _SIGS = {
     "cnmf_counter_words": (_i64, []),
     "cnmf_set_persist_variant": (_i32, [_i32]),
     "cnmf_get_persist_variant": (_i32, []),
+    "cnmf_set_persist_dyn_frac": (_i32, [ctypes.c_double]),
     "cnmf_counter_err_word": (_i32, []),
     "cnmf_mu_persistent": (_i32, [_i64, _i32, _i32, _i32]),
     "cnmf_als_table_doubles": (_i32, []),

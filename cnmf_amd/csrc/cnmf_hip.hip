@@ -1154,6 +1154,28 @@ __device__ __forceinline__ void sl_stage(unsigned char* smem, int wpar, const u3
   }
 }
 
+// the floating-tile (DYN) forms.  The same instruction sequence for every tile, static or floating
+// (runtime branches around the loads cost the compiler's waitcnt precision: ~0.6 µs per tile): X as in
+// sl_prefetch<false>, plus one 16-byte sc1 load per lane (two 8-byte agent-scope loads) that fetches
+// the tile's W when it floats (lanes 16..79) and otherwise re-reads the lane's first X chunk.
+// sc1 because a floating tile's W was stored sc1 by whichever workgroup (any XCD) processed it in the
+// previous iteration (MI355X_MICROARCH.md valid forms: sc1 stores, vmcnt(0), ticket, flag, sc1 loads).
+__device__ __forceinline__ void sl_prefetch_w(uint64_t (&pw)[2], const unsigned char* __restrict__ X,
+                                              const unsigned char* __restrict__ W, int64_t tile, bool flt, int t) {
+  // static tile: the lane's own first X chunk of the tile (just loaded by sl_prefetch, spread over
+  // the channels like X; a fixed line set shared by every workgroup serialised on one channel)
+  const unsigned char* src = flt ? W + (size_t)tile * WB + 16 * ((t - 16) & 63) : X + (size_t)tile * XB + 16 * t;
+  uint64_t* l = reinterpret_cast<uint64_t*>(const_cast<unsigned char*>(src));
+  pw[0] = __hip_atomic_load(l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  pw[1] = __hip_atomic_load(l + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void sl_stage_w(unsigned char* smem, int wpar, const uint64_t (&pw)[2], int t) {
+  if (t >= 16 && t < 80)  // a static tile's lanes write the unused W slot (never read)
+    *reinterpret_cast<u32x4*>(smem + L_W + wpar * WB + 16 * (t - 16)) =
+        u32x4{(unsigned)pw[0], (unsigned)(pw[0] >> 32), (unsigned)pw[1], (unsigned)(pw[1] >> 32)};
+}
+
 __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes are done
   __builtin_amdgcn_s_barrier();
@@ -1197,7 +1219,7 @@ __device__ __forceinline__ void phase1(unsigned char* smem, float (&xv)[NC], int
 // the new W written back to LDS; otherwise the staged tile is read and the new W stored to HBM.
 __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ W, int64_t tile, int wpar,
                                        int wave, int lane, double l1, double l2, float* wres = nullptr,
-                                       bool active = true) {
+                                       bool active = true, bool sc1w = false) {
   const double* sP = reinterpret_cast<const double*>(smem + L_P);
   const double* sHHt = reinterpret_cast<const double*>(smem + L_HHT);
   float* sWn = reinterpret_cast<float*>(smem + L_WN);
@@ -1221,9 +1243,10 @@ __device__ __forceinline__ void phase2(unsigned char* smem, float* __restrict__ 
   // inactive: a padding step of the team with one tile fewer (mu_iter_sl_kernel<…, 2>): nothing
   // is stored and w' = 0 makes phase 3 add nothing
   if (active) {
-    if (wres)
-      wres[s * K + j] = wn;  // the quad's float4 read above precedes this store (data dependence)
-    else
+    if (wres) wres[s * K + j] = wn;  // the quad's float4 read above precedes this store (data dependence)
+    if (sc1w)  // a floating tile: another workgroup (any XCD) reads this W next iteration
+      __hip_atomic_store(W + ((size_t)tile * TS + s) * K + j, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (!wres)
       W[((size_t)tile * TS + s) * K + j] = wn;
   }
   sWn[s * K + j] = active ? wn : 0.f;
@@ -1872,7 +1895,10 @@ constexpr int CNT_GROUP0 = 32;
 constexpr int CNT_TOP = CNT_GROUP0 + 32 * sl::MAX_GROUPS;
 constexpr int CNT_FLAG = CNT_TOP + 32;
 constexpr int CNT_ERR = CNT_FLAG + 32;
-constexpr int CNT_RCOL0 = CNT_ERR + 32;          // reduce_kernel: one ticket per 64-column block
+constexpr int DYN_GRP = 8;                       // workgroups per floating-tile pool
+constexpr int DYN_MAX_POOLS = sl::GROUP * sl::MAX_GROUPS / DYN_GRP;
+constexpr int CNT_POOL = CNT_ERR + 32;           // floating-tile pools [parity][pool] (32-word stride)
+constexpr int CNT_RCOL0 = CNT_POOL + 2 * DYN_MAX_POOLS * 32;          // reduce_kernel: one ticket per 64-column block
 constexpr int RED_MAX_COLS = 512;
 constexpr int CNT_WORDS = CNT_RCOL0 + RED_MAX_COLS;
 
@@ -1945,6 +1971,7 @@ struct PersistArgs {
   int64_t n_tiles;
   int n_iter;
   int n_groups;
+  int n_static;      // DYN: tiles per workgroup with W resident; tiles n_static*G.. float (the pool)
   double l1W, l2W, l1H, l2H;
   int apply_first;   // first apply the pending basis update from AB (multi-GPU: AB all-reduced)
   int apply_last;    // apply the last iteration's basis update in-launch (single GPU)
@@ -2050,10 +2077,22 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
 #define CNMF_TEAM_PRIO 1
 #endif
 constexpr bool SETPRIO = CNMF_TEAM_PRIO != 0;
-template <int PD, bool WRES, bool MULTI = false, int TEAMS = 1>
+//
+// DYN (floating tiles): each workgroup owns n_static tiles b + G·i (W resident, as above); the
+// remaining tiles form a pool that the workgroups draw from one at a time, every iteration, with an
+// agent-scope atomic counter (one per iteration parity).  A workgroup that streams faster takes more
+// of them, so the iteration no longer waits for the slowest CU's fixed share (the per-CU / per-XCD
+// spread of DESIGN.md §3.0).  A floating tile's W travels through HBM: sc1 loads and stores (the
+// next iteration's owner may sit on another XCD; the hand-off rides the iteration's tickets and
+// flag).  The draw for a position is issued one tile before it is needed (its latency hidden behind
+// a tile), before that tile's prefetch loads (so waiting for it never waits for them); thread 0
+// hands the result over through LDS.  The summation order then depends on the draw: results agree
+// with the static layouts to fp32 summation-order noise but are not bit-repeatable.
+template <int PD, bool WRES, bool MULTI = false, int TEAMS = 1, bool DYN = false>
 __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) void mu_iter_sl_kernel(PersistArgs a) {
   using namespace sl;
   static_assert(TEAMS == 1 || (TEAMS == 2 && PD == 2), "two teams: PD = 2");
+  static_assert(!DYN || (TEAMS == 1 && PD == 2 && WRES), "floating tiles: pairs, PD = 2, W resident");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_base[];
   const int tid = threadIdx.x;
   const int team = TEAMS == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 8);
@@ -2084,6 +2123,18 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
   uint32_t* cnt_top = a.cnt + CNT_TOP;
   uint32_t* flag = a.cnt + CNT_FLAG;
   uint32_t* err = a.cnt + CNT_ERR;
+  // DYN pools: workgroups 8p..8p+7 (consecutive, so on different XCDs) share pool p, which holds
+  // the floating tiles [f0, f1) (a share proportional to its workgroups); one counter per pool and
+  // iteration parity, so ~n_float/64 draws land on each address instead of all on one (draws on one
+  // address serialise at ~9 ns each: 4000 per iteration cost 37 µs)
+  const int S = DYN ? a.n_static : 0;
+  const int n_float = DYN ? (int)(a.n_tiles - (int64_t)S * G) : 0;
+  const int n_pools = (G + DYN_GRP - 1) / DYN_GRP;
+  const int my_pool = b / DYN_GRP;
+  const int f0 = DYN ? S * G + (int)((int64_t)n_float * (my_pool * DYN_GRP) / G) : 0;
+  const int f_n = DYN ? S * G + (int)((int64_t)n_float * min(my_pool * DYN_GRP + DYN_GRP, G) / G) - f0 : 0;
+  uint32_t* pool = a.cnt + CNT_POOL + 32 * my_pool;  // + 32·DYN_MAX_POOLS for odd iterations
+  const int n_res = DYN ? S : nbt_team;  // W tiles resident in LDS
 
   // ---- the basis for the first iteration
   for (int e = t; e < K * F; e += NT) sH[e] = a.H64[e];
@@ -2110,17 +2161,63 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
   };
   unsigned char* wres = smem + L_PTOTAL;  // [nbt][64][4] fp32 when WRES
   if (WRES) {
-    for (int c = t; c < nbt_team * (WB / 16); c += NT) {
+    for (int c = t; c < n_res * (WB / 16); c += NT) {
       const int i = c / (WB / 16), ch = c - i * (WB / 16);
       *reinterpret_cast<u32x4*>(wres + i * WB + 16 * ch) =
           *reinterpret_cast<const u32x4*>(Wb + (size_t)(vb + (int64_t)Gv * i) * WB + 16 * ch);
     }
   }
+  // DYN: the positions q, q+1, q+2 of this workgroup's tile sequence (tile, iteration, index in the
+  // iteration; it == n_iter: past the end) and the generator of the next positions
+  struct Pos {
+    int tile, it, i;
+  };
+  int gen_it = 0, gen_i = 0;
+  bool grab_pending = false;  // a draw was issued in the previous body (its value: thread 0's grab_reg)
+  uint32_t grab_reg = 0;
+  auto issue_grab = [&]() {
+    if (tid == 0)
+      grab_reg = __hip_atomic_fetch_add(pool + 32 * DYN_MAX_POOLS * (gen_it & 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    grab_pending = true;
+  };
+  auto produce = [&]() -> Pos {
+    if (gen_it >= a.n_iter) return Pos{0, a.n_iter, 0};
+    if (gen_i >= S) {  // a floating position: the draw issued one body ago (LDS word sFlag[3])
+      const uint32_t got = (uint32_t)__builtin_amdgcn_readfirstlane(sFlag[3]);
+      if (got < (uint32_t)f_n) {
+        const Pos p{f0 + (int)got, gen_it, gen_i};
+        ++gen_i;
+        issue_grab();
+        return p;
+      }
+      ++gen_it;  // the pool is empty: this workgroup's iteration ends here
+      gen_i = 0;
+      if (gen_it >= a.n_iter) return Pos{0, a.n_iter, 0};
+    }
+    const Pos p{b + G * gen_i, gen_it, gen_i};
+    ++gen_i;
+    if (gen_i == S) issue_grab();
+    return p;
+  };
+  Pos P0{0, 0, 0}, P1{0, 0, 0}, P2{0, 0, 0};
   u32x4 pfA[PFN], pfB[PFN];
-  sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(0), t);
-  if (PD == 2 && total > 1) sl_prefetch<!WRES>(pfB, Xb, Wb, tile_at(1), t);
-  sl_stage<!WRES>(smem, 0, pfA, t);
-  if (total > PD) sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
+  uint64_t pwA[2] = {0, 0}, pwB[2] = {0, 0};  // DYN: the W chunk of the tile in pfA / pfB
+  if (DYN) {
+    P0 = produce();
+    P1 = produce();
+    P2 = produce();  // S >= PD + 2: all static
+    sl_prefetch<false>(pfA, Xb, Wb, P0.tile, t);
+    sl_prefetch<false>(pfB, Xb, Wb, P1.tile, t);
+    sl_prefetch_w(pwB, Xb, Wb, P1.tile, false, t);
+    sl_stage<false>(smem, 0, pfA, t);
+    sl_prefetch<false>(pfA, Xb, Wb, P2.tile, t);
+    sl_prefetch_w(pwA, Xb, Wb, P2.tile, false, t);
+  } else {
+    sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(0), t);
+    if (PD == 2 && total > 1) sl_prefetch<!WRES>(pfB, Xb, Wb, tile_at(1), t);
+    sl_stage<!WRES>(smem, 0, pfA, t);
+    if (total > PD) sl_prefetch<!WRES>(pfA, Xb, Wb, tile_at(PD == 1 ? 1 : 2), t);
+  }
   lds_barrier();
   TL_START;
   // the second-dispatched half (waves 4-7) loses every VALU arbitration to its older SIMD partner
@@ -2130,14 +2227,16 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
 
   bool alive = true;
   int wpar = 0;
-  auto body = [&](int q, u32x4 (&pf)[PFN]) {
-    const int it = q / nbt;
-    const int i = q - it * nbt;
-    const bool end_it = i + 1 == nbt;
+  auto body = [&](int q, u32x4 (&pf)[PFN], uint64_t (&pw)[2]) {
+    const int it = DYN ? P0.it : q / nbt;
+    const int i = DYN ? P0.i : q - it * nbt;
+    const bool end_it = DYN ? P1.it != P0.it : i + 1 == nbt;
     const bool last_it = it + 1 == a.n_iter;
-    const bool has1 = q + 1 < total;
-    const bool hasP = q + 1 + PD < total;
-    const int64_t tile = tile_at(q);
+    const bool has1 = DYN ? P1.it < a.n_iter : q + 1 < total;
+    const bool hasP = DYN ? true : q + 1 + PD < total;
+    const int64_t tile = DYN ? (int64_t)P0.tile : tile_at(q);
+    const bool flt = DYN && i >= S;  // a floating tile: W staged from HBM, stored sc1
+    const bool flt1 = DYN && P1.i >= S;
     float xv[NC];
     // two teams run half a tile apart: team 1 passes one barrier before its first tile of the
     // iteration and team 0 one after its last, so team 1's phase 1 overlaps team 0's phase 2 and
@@ -2149,10 +2248,38 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
     if (!WRES) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     lds_barrier();  // A
     phase2(smem, a.W, tile, wpar, wave, lane, a.l1W, a.l2W,
-           WRES ? reinterpret_cast<float*>(wres + i * WB) : nullptr, TEAMS == 1 || i < nbt_team);
-    if (has1) sl_stage<!WRES>(smem, wpar ^ 1, pf, t);
-    if (hasP && !end_it) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);
+           // DYN: a floating tile's W is read from (and its update also written to) its staging slot
+           DYN ? reinterpret_cast<float*>(flt ? smem + L_W + wpar * WB : wres + i * WB)
+               : (WRES ? reinterpret_cast<float*>(wres + i * WB) : nullptr),
+           TEAMS == 1 || i < nbt_team, flt);
+    if (DYN) {
+      if (has1) {
+        sl_stage<false>(smem, wpar ^ 1, pf, t);
+        sl_stage_w(smem, wpar ^ 1, pw, t);
+      }
+      // the draw issued in the previous body -> LDS, here where the stage has already waited for
+      // the loads issued before it (a wait for the draw's value elsewhere in the body costs the
+      // compiler's conservative vmcnt(0): the whole prefetch, ~0.8 µs per tile)
+      if (grab_pending) {
+        if (tid == 0) sFlag[3] = (int)grab_reg;
+        grab_pending = false;
+      }
+    } else {
+      if (has1) sl_stage<!WRES>(smem, wpar ^ 1, pf, t);
+      if (hasP && !end_it) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);
+    }
     lds_barrier();  // B
+    if (DYN) {  // position q + 1 + PD: its draw (if floating) read from LDS, the next draw issued
+      const Pos P3 = produce();
+      // at the iteration's end the prefetch waits until the row's vmcnt(0) below has passed
+      if (!end_it && P3.it < a.n_iter) {
+        sl_prefetch<false>(pf, Xb, Wb, P3.tile, t);
+        sl_prefetch_w(pw, Xb, Wb, P3.tile, P3.i >= S, t);
+      }
+      P0 = P1;
+      P1 = P2;
+      P2 = P3;
+    }
     phase3(smem, xv, acc, acc33, wave, lane);
     wpar ^= 1;
     if (!end_it) return;
@@ -2169,7 +2296,15 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
     acc33 = 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
     __syncthreads();
-    if (hasP) sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);  // in flight during the reduction
+    // in flight during the reduction (DYN: P2 is now position q + 1 + PD)
+    if (DYN) {
+      if (P2.it < a.n_iter) {
+        sl_prefetch<false>(pf, Xb, Wb, P2.tile, t);
+        sl_prefetch_w(pw, Xb, Wb, P2.tile, P2.i >= S, t);
+      }
+    } else if (hasP) {
+      sl_prefetch<!WRES>(pf, Xb, Wb, tile_at(q + 1 + PD), t);
+    }
     TL(it, 0);
     if (tid == 0) {
       const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2288,6 +2423,11 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
         }
       }
       if (sFlag[1]) {
+        // this iteration's pool is drained (every workgroup's failed draw precedes its ticket):
+        // ready for iteration it + 2
+        if (DYN && tid < n_pools)
+          __hip_atomic_store(a.cnt + CNT_POOL + 32 * (DYN_MAX_POOLS * (it & 1) + tid), 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0 && !last_it)
@@ -2304,7 +2444,7 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
     if (last_it) {
       alive = false;
       if (WRES) {  // this team's W back to HBM, once per launch
-        for (int c = t; c < nbt_team * (WB / 16); c += NT) {
+        for (int c = t; c < n_res * (WB / 16); c += NT) {
           const int ii = c / (WB / 16), ch = c - ii * (WB / 16);
           *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(vb + (int64_t)Gv * ii) * WB + 16 * ch) =
               *reinterpret_cast<const u32x4*>(wres + ii * WB + 16 * ch);
@@ -2359,10 +2499,17 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
     TL(it, 1);
   };
 
-  for (int q = 0; q < total && alive; q += 2) {
-    if (PD == 1) body(q, pfA);
-    else body(q, pfB);
-    if (q + 1 < total && alive) body(q + 1, pfA);
+  if (DYN) {
+    for (int q = 0; alive; q += 2) {  // ends at the last iteration's end (or an error)
+      body(q, pfB, pwB);
+      if (alive) body(q + 1, pfA, pwA);
+    }
+  } else {
+    for (int q = 0; q < total && alive; q += 2) {
+      if (PD == 1) body(q, pfA, pwA);
+      else body(q, pfB, pwB);
+      if (q + 1 < total && alive) body(q + 1, pfA, pwA);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
 }
@@ -3385,11 +3532,15 @@ static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
 // 66.5 µs on one, 70.2 vs 67.3 µs on another), so it is a process-wide switch the host can set
 // after timing both (MUPlan.tune): 1 = pairs of 4-wave workgroups (the default), 2 = two teams.
 // CNMF_TEAMS=1|2 sets the initial value.
-static std::atomic<int> g_persist_variant{
-    (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 1};
+static int initial_variant() {
+  const char* v = getenv("CNMF_PERSIST_VARIANT");
+  if (v && (atoi(v) == 2 || atoi(v) == 3)) return atoi(v);
+  return (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 1;
+}
+static std::atomic<int> g_persist_variant{initial_variant()};
 
 int cnmf_set_persist_variant(int v) {
-  if (v != 1 && v != 2) return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs) or 2 (teams)");
+  if (v < 1 || v > 3) return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs), 2 (teams) or 3 (pairs + floating tiles)");
   g_persist_variant.store(v);
   return CNMF_OK;
 }
@@ -3397,6 +3548,35 @@ int cnmf_get_persist_variant(void) { return g_persist_variant.load(); }
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 2>);
+}
+
+// ---- variant 3: pairs with floating tiles (mu_iter_sl_kernel<2, true, MULTI, 1, true>): each
+// workgroup keeps floor(frac · n_tiles / G) tiles resident (frac = CNMF_DYN_FRAC, default 0.8), the
+// rest are drawn from a pool every iteration.  Returns the static tiles per workgroup (0: not
+// eligible) and the LDS bytes.
+static std::atomic<double> g_dyn_frac{getenv("CNMF_DYN_FRAC") ? atof(getenv("CNMF_DYN_FRAC")) : 0.8};
+int cnmf_set_persist_dyn_frac(double frac) {
+  if (!(frac > 0.0 && frac <= 1.0)) return set_err(CNMF_ERR_ARG, "frac must lie in (0, 1]");
+  g_dyn_frac = frac;
+  return CNMF_OK;
+}
+static bool g_dyn_multi = getenv("CNMF_DYN_MULTI") && strcmp(getenv("CNMF_DYN_MULTI"), "1") == 0;
+static PassFn persist_dyn_fn(bool multi) {
+  return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 1, true>)
+               : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 1, true>);
+}
+static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, size_t* lds_out) {
+  if (g_persist_variant.load() != 3 || g_no_wres || g_persist_pd != 2 || G <= 0) return 0;
+  if (multi && !g_dyn_multi) return 0;  // the multi-GPU launch keeps layout 1 unless CNMF_DYN_MULTI=1
+  const double fr = g_dyn_frac.load();
+  const double frac = fr > 0.0 && fr <= 1.0 ? fr : 0.8;
+  const int64_t S = (int64_t)(frac * (double)n_tiles / (double)G);
+  if (S < 4 || S * G > n_tiles) return 0;  // >= PD + 2 static tiles (no draw crosses an iteration)
+  const size_t lds = (size_t)sl::L_PTOTAL + (size_t)S * sl::WB;
+  if (lds > kMaxLds) return 0;
+  if (max_resident(persist_dyn_fn(multi), lds) < G) return 0;  // the whole grid co-resident
+  *lds_out = lds;
+  return (int)S;
 }
 
 // workgroups (0: not eligible) and LDS bytes of a two-team launch over n_tiles (persist_grid > 0)
@@ -3510,6 +3690,7 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.n_tiles = n_rows / TS;
   pa.n_iter = n_iter;
   pa.n_groups = (int)((G + sl::GROUP - 1) / sl::GROUP);
+  pa.n_static = 0;
   pa.l1W = l1_W;
   pa.l2W = l2_W;
   pa.l1H = l1_H;
@@ -3525,6 +3706,13 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
     if (GT > 0 && GT <= n_parts) {
       pa.n_groups = (int)((GT + sl::GROUP - 1) / sl::GROUP);
       HIP_CHECK(hipLaunchKernel(persist_teams_fn(multi), dim3((unsigned)GT), dim3(2 * NT), args, tlds, s));
+      return CNMF_OK;
+    }
+    size_t dlds = 0;
+    const int S = persist_dyn_static(n_rows / TS, G, multi, &dlds);
+    if (S > 0) {
+      pa.n_static = S;
+      HIP_CHECK(hipLaunchKernel(persist_dyn_fn(multi), dim3((unsigned)G), dim3(NT), args, dlds, s));
       return CNMF_OK;
     }
   }
@@ -3569,6 +3757,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     pa.n_tiles = n_rows / TS;
     pa.n_iter = 1;
     pa.n_groups = (int)((G + sl::GROUP - 1) / sl::GROUP);
+    pa.n_static = 0;
     pa.l1W = l1_W;
     pa.l2W = l2_W;
     pa.l1H = l1_H;

@@ -242,7 +242,7 @@ class MUPlan:
         synchronises the stream."""
         if getattr(self, "persistent", False) and int(self.counter[self.err_word].item()) != 0:
             code = int(self.counter[self.err_word].item())
-            self.counter[self.err_word] = 0
+            self.counter.zero_()  # tickets, pools and the error word: at rest for the next launch
             if getattr(self, "exchange", False):
                 self.disable_exchange()  # the buffer set's flags are poisoned: never reuse it
                 raise _lib.HipLibraryError(
@@ -294,19 +294,20 @@ class MUPlan:
         self.basis_update()
 
     def tune(self, n_iter: int = 100, rounds: int = 2) -> dict:
-        """Time both layouts of the persistent launch (cnmf_set_persist_variant: 1 = pairs of
-        4-wave workgroups, 2 = 8-wave two-team workgroups) on this plan's shape and keep the faster
-        one for the process.  Runs on copies of W and H: the plan's state is unchanged.  Call after
+        """Time the layouts of the persistent launch (cnmf_set_persist_variant: 1 = pairs of
+        4-wave workgroups, 2 = 8-wave two-team workgroups, 3 = pairs with floating tiles) on this
+        plan's shape and keep the fastest for the process.  Runs on copies of W and H: the plan's state is unchanged.  Call after
         the GPU has been busy for a while (the clock ramps up over the first ~35 ms of work).
         Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent plans."""
         if not self.persistent:
             return {}
         W0, H0 = self.W.clone(), self.H64.clone()
         stream = torch.cuda.current_stream(self.device)
-        times = {1: [], 2: []}
+        variants = (1, 2, 3)
+        times = {v: [] for v in variants}
         try:
             for _ in range(rounds):
-                for v in (1, 2):
+                for v in variants:
                     check(self.lib.cnmf_set_persist_variant(v), "cnmf_set_persist_variant")
                     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                     ev[0].record(stream)

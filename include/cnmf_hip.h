@@ -107,10 +107,15 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
 
 /* Process-wide layout of multi-iteration persistent launches (results agree to fp32 rounding of
  * the per-workgroup partial sums, not bit for bit): 1 = two independent 4-wave workgroups per CU
- * (default), 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart.
- * The faster one differs between boxes; MUPlan.tune() times both and sets it. */
+ * (default), 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart,
+ * 3 = layout 1 with floating tiles: a fraction `frac` of the tiles stays with its workgroup (W
+ * resident), the rest is drawn from a pool every iteration so that faster CUs take more (not
+ * bit-repeatable: the draw decides the summation order).  The fastest differs between boxes;
+ * MUPlan.tune() times them and sets it.  cnmf_set_persist_dyn_frac: frac in (0, 1] (default 0.8,
+ * env CNMF_DYN_FRAC); a shape with fewer than 4 static tiles per workgroup uses layout 1. */
 int cnmf_set_persist_variant(int variant);
 int cnmf_get_persist_variant(void);
+int cnmf_set_persist_dyn_frac(double frac);
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
  * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction

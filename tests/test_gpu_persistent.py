@@ -35,10 +35,12 @@ def _unfused(plan, n):
         plan.basis_update()
 
 
-@pytest.fixture(params=[1, 2], ids=["pairs", "teams"])
+@pytest.fixture(params=[1, 2, 3], ids=["pairs", "teams", "floating"])
 def layout(request):
-    """The persistent launch's two layouts (cnmf_set_persist_variant): pairs of 4-wave workgroups
-    per CU, or one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart)."""
+    """The persistent launch's layouts (cnmf_set_persist_variant): pairs of 4-wave workgroups per
+    CU, one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart), or pairs with
+    floating tiles (a pool drawn every iteration; shapes with < 4 static tiles per workgroup fall
+    back to pairs)."""
     from cnmf_amd import _lib
     lib = _lib.load()
     old = lib.cnmf_get_persist_variant()
@@ -144,3 +146,43 @@ def test_persistent_tol_stop_through_api():
                                max_iter=400, tol=1e-4)
     assert n == nr
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32
+
+
+# (tiles, frac): no floating tile at all (every workgroup's one draw fails), the minimum of 4 static
+# tiles with half the tiles floating, cfg2's tile count at the default fraction, a ragged count
+@pytest.mark.parametrize("n_tiles,frac", [(4096, 1.0), (4096, 0.5), (15625, 0.8), (3001, 0.7)])
+def test_floating_tiles(n_tiles, frac):
+    """Layout 3: tiles drawn from a pool every iteration, their W handed between workgroups (and
+    XCDs) through HBM.  Every tile must be updated exactly once per iteration: the factors match the
+    oracle and the static layout (to fp32 summation-order noise), across split launches too, and the
+    counters (tickets and both pools) are back at rest."""
+    from cnmf_amd import _lib
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    lib = _lib.load()
+    old = lib.cnmf_get_persist_variant()
+    X = iop_spectra(64 * n_tiles, 81, seed=n_tiles + 3, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 11)
+    n_it = 60 if n_tiles < 15625 else 30
+    try:
+        assert lib.cnmf_set_persist_dyn_frac(frac) == 0
+        lib.cnmf_set_persist_variant(1)
+        ref = _plan(X, W0, H0)
+        ref.iterate(n_it)
+        lib.cnmf_set_persist_variant(3)
+        a, c = _plan(X, W0, H0), _plan(X, W0, H0)
+        a.iterate(n_it)
+        for n in (2, n_it // 2 - 2, n_it - n_it // 2):
+            c.iterate(n)
+        for p in (a, c):
+            p.check_sync_error()
+            assert int(p.counter.cpu().numpy().astype(np.int64).sum()) == 0
+    finally:
+        lib.cnmf_set_persist_dyn_frac(0.8)
+        lib.cnmf_set_persist_variant(old)
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=n_it, tol=0.0)
+    for p in (a, c):
+        W, H = p.W.cpu().numpy(), p.H64.cpu().numpy()
+        assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+        assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6 and rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
+    assert lib.cnmf_set_persist_dyn_frac(0.0) != 0 and lib.cnmf_set_persist_dyn_frac(1.5) != 0

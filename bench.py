@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
     p.add_argument("--cpu-seconds", type=float, default=15.0, help="budget of the CPU baseline")
     p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--weighted", action="store_true",
+                   help="the weighted / masked MU (SURVEY §8(f) row 2): synthetic weights, 30 %% zero")
     p.add_argument("--solver", default="mu", choices=["mu", "als"],
                    help="mu: cfg2 (the headline); als: cfg5, the constrained ALS")
     p.add_argument("--sum-to-one", type=float, default=1.0, help="ALS sum-to-one weight (delta)")
@@ -205,7 +207,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from cnmf_amd.solver import ALSPlan, MUPlan
+    from cnmf_amd.solver import ALSPlan, MUPlan, WeightedMUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
 
     n_rows, F, k = args.rows, args.features, args.k
@@ -219,23 +221,27 @@ def main():
     H0d = torch.from_numpy(H0).to(dev)
     if world > 1:
         dist.broadcast(H0d, src=0)
-    if args.solver == "als":
+    if args.weighted:
+        rng = np.random.default_rng(rank)
+        Mw = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)
+        plan = WeightedMUPlan(Xd, torch.from_numpy(Mw).to(dev), k)
+    elif args.solver == "als":
         plan = ALSPlan(Xd, k, sum_to_one=args.sum_to_one, smoothness=args.smoothness)
     else:
         plan = MUPlan(Xd, k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     exchange = None
-    if args.solver == "mu" and dist_path and args.exchange == "auto" and plan.persistent_shape:
+    if args.solver == "mu" and not args.weighted and dist_path and args.exchange == "auto" and plan.persistent_shape:
         exchange = validate_exchange(plan, W0, H0d)
         print(f"[rank {rank}] in-launch exchange: {exchange}", file=sys.stderr, flush=True)
-    elif args.dist and args.solver == "mu":
+    elif args.dist and args.solver == "mu" and not args.weighted:
         plan.use_shard_steps()
     torch.cuda.synchronize()
 
     plan.iterate(args.warmup)
     torch.cuda.synchronize()
-    if plan.exchange:  # a failed warmup launch falls back before anything is timed
+    if getattr(plan, "exchange", False):  # a failed warmup launch falls back before anything is timed
         fail = torch.zeros(1, dtype=torch.float64, device=dev)
         try:
             plan.check_sync_error()
@@ -284,7 +290,7 @@ def main():
         return persistent, events, elapsed
 
     persistent, events, elapsed = timed()
-    if plan.exchange:  # a failed exchange launch: every rank re-times on RCCL
+    if getattr(plan, "exchange", False):  # a failed exchange launch: every rank re-times on RCCL
         fail = torch.zeros(1, dtype=torch.float64, device=dev)
         try:
             plan.check_sync_error()
@@ -317,7 +323,7 @@ def main():
 
     sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
     sw = 8 if args.dtype == "f64" else 4
-    bytes_per_pass = n_rows * (F * sx + 2 * k * sw)
+    bytes_per_pass = n_rows * (F * sx + 2 * k * sw) + (n_rows * F * 4 if args.weighted else 0)  # + M
     iters_per_launch = K if persistent else 1
     bytes_per_launch = bytes_per_pass * iters_per_launch
     achieved = bytes_per_launch / avg_pass_s / 1e9
@@ -331,10 +337,12 @@ def main():
             dist.destroy_process_group()
         return
 
-    traffic, traffic_src = (None, None) if args.solver == "als" else load_traffic(args.traffic_json, n_rows, F, k)
+    traffic, traffic_src = (None, None) if (args.solver == "als" or args.weighted) else load_traffic(args.traffic_json, n_rows, F, k)
     if traffic is not None:
         traffic = traffic * iters_per_launch
-    if args.solver == "als":
+    if args.weighted:
+        kname = "weighted MU pass (wmu_pass_kernel: W-step + [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))])"
+    elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
     elif persistent and world == 1:
         kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
@@ -358,7 +366,7 @@ def main():
                 "max_over_ranks_avg_launch_us": round(avg_pass_s_max * 1e6, 2)}
 
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and not args.weighted:
         Xc = X if args.dtype != "bf16" else Xt.float().numpy()
         if args.solver == "als":
             cpu = cpu_baseline_als(Xc, W0, H0, args.sum_to_one, args.smoothness, args.cpu_seconds)
@@ -367,7 +375,11 @@ def main():
 
     total_units = world * n_rows / 1e6
     value = total_units * K / elapsed
-    if args.solver == "als":
+    if args.weighted:
+        metric = "weighted MU iterations/sec (V=1e6x81 k=4 with per-element weights, 30 % zero)"
+        workload = (f"weighted / masked MU (SURVEY 8f row 2, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+                    f"f32 synthetic IOP spectra, synthetic weights U(0.2, 2) with 30 % zeros")
+    elif args.solver == "als":
         metric = ("constrained-ALS iterations/sec (cfg5: V=1e6x81 k=4, sum-to-one + smoothness) & "
                   "achieved HBM GB/s of the W-step pass vs peak")
         workload = (f"cfg5: constrained ALS (FCLS W-step delta={args.sum_to_one}, smoothness "
@@ -398,7 +410,7 @@ def main():
                                   + (", in-launch over xGMI)" if plan.exchange else ", RCCL)")
                                   + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
                    "exchange": exchange,
-                   "persistent_layout": layout,
+                   "persistent_layout": layout if plan.persistent else None,
                    "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -165,14 +165,37 @@ def _validate_als(solver, alpha_W, alpha_H, sum_to_one, smoothness):
                              f"Got {v!r} instead.")
 
 
+def _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise):
+    """Weighted / masked MU: per-element weights of X's shape, finite and
+    non-negative, float32 X; solver 'mu' without alpha regularisation or normalise."""
+    if weights is None:
+        return None
+    if solver != "mu":
+        raise ValueError("weights apply to solver='mu' only")
+    if alpha_W != 0 or alpha_H not in ("same", 0, 0.0):
+        raise ValueError("the weighted MU takes no alpha_W / alpha_H regularisation")
+    if normalise is not None:
+        raise ValueError("normalise is not supported together with weights")
+    Mw = _check_X(weights)
+    if tuple(Mw.shape) != tuple(X.shape):
+        raise ValueError(f"weights must have X's shape {tuple(X.shape)}, got {tuple(Mw.shape)}")
+    if _min(Mw) < 0:
+        raise ValueError("Negative values in data passed to NMF (input weights)")
+    torch = _torch()
+    if (_is_torch(X) and X.dtype != torch.float32) or (not _is_torch(X) and X.dtype != np.float32):
+        raise TypeError("the weighted MU runs in float32: pass X (and W, H) as float32")
+    return Mw
+
+
 def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                    l1_ratio, random_state, verbose, device, group=None, return_plan=False,
-                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0):
+                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None):
     """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
     torch = _torch()
-    from .solver import ALSPlan, MUPlan, run_mu
+    from .solver import ALSPlan, MUPlan, WeightedMUPlan, run_mu
 
     X = _check_X(X)
+    Mw = _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise)
     as_torch = _is_torch(X)
     n_samples, n_features = X.shape
     k = n_components
@@ -221,7 +244,12 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
     dev = torch.device(device) if device is not None else (X.device if as_torch else torch.device("cuda", torch.cuda.current_device()))
     Xd = X if as_torch else torch.from_numpy(X)
     Xd = Xd.to(dev, non_blocking=False).contiguous()
-    if solver == "als":
+    if Mw is not None:
+        if k > 8:
+            raise ValueError(f"n_components={k} is not supported by the weighted MU (1..8).")
+        Md = (Mw if _is_torch(Mw) else torch.from_numpy(Mw)).to(dev, torch.float32).contiguous()
+        plan = WeightedMUPlan(Xd, Md, k, group=group)
+    elif solver == "als":
         plan = ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
     else:
         plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
@@ -255,7 +283,7 @@ def _out(t, as_torch, X):
 def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
               beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
               l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None,
-              normalise=None, sum_to_one=None, smoothness=0.0):
+              normalise=None, sum_to_one=None, smoothness=0.0, weights=None):
     """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
@@ -268,13 +296,18 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
     non-negative least squares with a sum-to-one penalty of weight `sum_to_one` (δ; None = off),
     and per basis row the exact NNLS with a second-difference smoothness penalty `smoothness` (λ)
     — see oracle/als_ref.py for the precise objective.  tol / max_iter work as for 'mu'.
+    `weights` (array of X's shape, >= 0; None = off) selects the weighted / masked MU (SURVEY.md
+    §8(f) row 2, oracle/wmu_ref.py): the loss becomes Σ m·(x − wh)², so a weight 0 marks a missing
+    value (give X any finite non-negative entry there) and 1/σ² an uncertainty weight; float32 X,
+    k <= 8, no alpha regularisation; tol tests the weighted error.
     """
     _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
     _validate_normalise(normalise)
     _validate_als(solver, alpha_W, alpha_H, sum_to_one, smoothness)
     return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                           l1_ratio, random_state, verbose, device, normalise=normalise,
-                          solver=solver, sum_to_one=sum_to_one, smoothness=smoothness)
+                          solver=solver, sum_to_one=sum_to_one, smoothness=smoothness,
+                          weights=weights)
 
 
 def _validate_normalise(normalise):
@@ -332,14 +365,15 @@ class NMF:
         _validate_normalise(self.normalise)
         _validate_als(self.solver, self.alpha_W, self.alpha_H, self.sum_to_one, self.smoothness)
 
-    def fit_transform(self, X, y=None, W=None, H=None):
-        """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H."""
+    def fit_transform(self, X, y=None, W=None, H=None, weights=None):
+        """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H
+        (the weighted error when `weights` is given: see `factorise`)."""
         self._validate()
         Wd, Hd, n_iter, plan, as_torch, Xc = _fit_transform(
             X, W, H, self.n_components, self.init, True, self.tol, self.max_iter, self.alpha_W,
             self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
             return_plan=True, normalise=self.normalise, solver=self.solver,
-            sum_to_one=self.sum_to_one, smoothness=self.smoothness)
+            sum_to_one=self.sum_to_one, smoothness=self.smoothness, weights=weights)
         self.reconstruction_err_ = plan.frobenius_error()
         self.n_components_ = int(Hd.shape[0])
         self.components_ = _out(Hd, as_torch, Xc)

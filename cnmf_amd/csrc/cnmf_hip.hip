@@ -3139,6 +3139,217 @@ static size_t reduce_lds(int n_out, int fuse, int F, int k) {
 
 using namespace cnmf;
 
+
+// ------------------------------------------------------------------------------------------------
+// Weighted / masked MU (spec + oracle: oracle/wmu_ref.py).  Per-element
+// weights M >= 0 (0 = a missing value, 1/σ² = an uncertainty weight):
+//   W <- W ∘ ((M∘X)·Hᵀ) / ((M∘(W·H))·Hᵀ)        H <- H ∘ (W'ᵀ·(M∘X)) / (W'ᵀ·(M∘(W'·H)))
+// in the order of SK:831-870 (W-step first; the H-step uses the new W'), zero denominators ->
+// EPS32 as SK:620/706.  With M = 1 both reduce to SK's Frobenius MU.
+//
+// One HBM pass per iteration: X and M once (8 bytes per element) plus W read + written.  Unlike
+// the unweighted update the W denominator does not factor through HHᵀ (M couples the features),
+// so phase 1 forms the reconstruction w·h_f per element.  Per tile of `ts` samples (staged in LDS):
+//   phase 1  P = 256/ts lanes per sample, features strided by P (consecutive lanes -> consecutive
+//            features), fp64: rec = w·h_f, num_j += m·x·h_jf, den_j += m·rec·h_jf; xor-shuffle
+//            sums over the P lanes; the part-0 lane writes w' (HBM and LDS)
+//   phase 2  thread = feature: over the tile's samples rec' = w'·h_f, A_j += w'_j·m·x,
+//            D_j += w'_j·m·rec' in fp32, folded into fp64 registers once per tile
+// Each workgroup writes one fp64 row [A | D] (2kF) at the end; cnmf_reduce_partials sums the rows
+// in fixed order and cnmf_wmu_basis_update applies the H-step.  Loss pass: Σ m·(x − w·h)² in fp64.
+// Limits: k <= 8, F <= 512 (registers of phase 2: NFT features per thread).
+// ------------------------------------------------------------------------------------------------
+template <int KP, int NFT>
+__global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ X, const float* __restrict__ M,
+                                                      float* __restrict__ W, const double* __restrict__ H64,
+                                                      double* __restrict__ partials, int64_t n_rows, int F,
+                                                      int k, int ts, int flags, int64_t n_tiles) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);  // [ts][F]
+  float* sM = sX + ts * F;                     // [ts][F]
+  float* sH = sM + ts * F;                     // [KP][F] (rows >= k zero)
+  float* sWn = sH + KP * F;                    // [ts][KP] the tile's new W
+  double* sRed = reinterpret_cast<double*>(smem + ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
+  const bool do_upd = (flags & CNMF_PASS_UPDATE_W) != 0;
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+  const int P = NT / ts;  // lanes per sample in phase 1 (a power of two <= 64)
+  const int sp = t / P;
+  const int part = t - sp * P;
+  for (int e = t; e < KP * F; e += NT) sH[e] = e < k * F ? (float)H64[e] : 0.f;
+  __syncthreads();
+  float hf[NFT][KP];
+  double A64[NFT][KP], D64[NFT][KP];
+#pragma unroll
+  for (int u = 0; u < NFT; ++u) {
+    const int f = t + NT * u;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      hf[u][j] = f < F ? sH[j * F + f] : 0.f;
+      A64[u][j] = 0.0;
+      D64[u][j] = 0.0;
+    }
+  }
+  double loss = 0.0;
+  for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    const int64_t r0 = tile * ts;
+    const int ns = (int)min<int64_t>(ts, n_rows - r0);
+    __syncthreads();  // the previous tile's phase 2 is done with sX / sM / sWn
+    {
+      const float* xs = X + r0 * F;
+      const float* ms = M + r0 * F;
+      for (int e = t; e < ns * F; e += NT) {  // the tile's rows are one contiguous span
+        sX[e] = xs[e];
+        sM[e] = ms[e];
+      }
+    }
+    __syncthreads();
+    // ---- phase 1
+    {
+      const bool valid = sp < ns;
+      double w[KP];
+#pragma unroll
+      for (int j = 0; j < KP; ++j) w[j] = (valid && j < k) ? (double)W[(r0 + sp) * k + j] : 0.0;
+      double num[KP], den[KP], l = 0.0;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) num[j] = den[j] = 0.0;
+      if (valid) {
+        const float* xr = sX + sp * F;
+        const float* mr = sM + sp * F;
+        for (int f = part; f < F; f += P) {
+          const double x = (double)xr[f];
+          const double m = (double)mr[f];
+          double rec = 0.0;
+#pragma unroll
+          for (int j = 0; j < KP; ++j) rec = fma(w[j], (double)sH[j * F + f], rec);
+          if (do_loss) {
+            const double r = x - rec;
+            l = fma(m * r, r, l);
+          } else {
+            const double mx = m * x, mrec = m * rec;
+#pragma unroll
+            for (int j = 0; j < KP; ++j) {
+              const double h = (double)sH[j * F + f];
+              num[j] = fma(mx, h, num[j]);
+              den[j] = fma(mrec, h, den[j]);
+            }
+          }
+        }
+      }
+      for (int off = 1; off < P; off <<= 1) {  // the sample's P lanes are consecutive
+        l += __shfl_xor(l, off);
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+          num[j] += __shfl_xor(num[j], off);
+          den[j] += __shfl_xor(den[j], off);
+        }
+      }
+      if (do_loss) {
+        if (part == 0 && valid) loss += l;
+      } else if (part == 0 && sp < ts) {
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+          float wn = 0.f;
+          if (valid && j < k) {
+            if (do_upd) {
+              double d = den[j];
+              if (d == 0.0) d = EPS32;  // SK:620
+              wn = (float)(w[j] * (num[j] / d));
+              W[(r0 + sp) * k + j] = wn;
+            } else {
+              wn = (float)w[j];
+            }
+          }
+          sWn[sp * KP + j] = wn;
+        }
+      }
+    }
+    if (!do_acc) continue;
+    __syncthreads();
+    // ---- phase 2
+#pragma unroll
+    for (int u = 0; u < NFT; ++u) {
+      const int f = t + NT * u;
+      if (f < F) {
+        float a32[KP], d32[KP];
+#pragma unroll
+        for (int j = 0; j < KP; ++j) a32[j] = d32[j] = 0.f;
+        for (int s2 = 0; s2 < ns; ++s2) {
+          const float x = sX[s2 * F + f];
+          const float m = sM[s2 * F + f];
+          float wr[KP];
+#pragma unroll
+          for (int j = 0; j < KP; j += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(sWn + s2 * KP + j);
+            wr[j] = v.x;
+            wr[j + 1] = v.y;
+            wr[j + 2] = v.z;
+            wr[j + 3] = v.w;
+          }
+          float rec = 0.f;
+#pragma unroll
+          for (int j = 0; j < KP; ++j) rec = fmaf(wr[j], hf[u][j], rec);
+          const float mx = m * x, mrec = m * rec;
+#pragma unroll
+          for (int j = 0; j < KP; ++j) {
+            a32[j] = fmaf(wr[j], mx, a32[j]);
+            d32[j] = fmaf(wr[j], mrec, d32[j]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < KP; ++j) {
+          A64[u][j] += (double)a32[j];
+          D64[u][j] += (double)d32[j];
+        }
+      }
+    }
+  }
+  if (do_loss) {  // the workgroup's Σ: waves by shuffles, then the 4 wave sums in order
+    for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
+    if (lane == 0) sRed[t >> 6] = loss;
+    __syncthreads();
+    if (t == 0) partials[blockIdx.x] = (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+    return;
+  }
+  if (!do_acc) return;
+  double* prow = partials + (size_t)blockIdx.x * (2 * k * F);
+#pragma unroll
+  for (int u = 0; u < NFT; ++u) {
+    const int f = t + NT * u;
+    if (f < F)
+#pragma unroll
+      for (int j = 0; j < KP; ++j)
+        if (j < k) {
+          prow[j * F + f] = A64[u][j];
+          prow[k * F + j * F + f] = D64[u][j];
+        }
+  }
+}
+
+// H <- H ∘ A / D (D == 0 -> EPS32, SK:706), AD = [A | D] reduced over all samples (and ranks)
+__global__ __launch_bounds__(256) void wmu_basis_kernel(const double* __restrict__ AD, double* __restrict__ H64, int kF) {
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < kF; e += gridDim.x * 256) {
+    double d = AD[kF + e];
+    if (d == 0.0) d = EPS32;
+    H64[e] = H64[e] * (AD[e] / d);
+  }
+}
+
+// tile size of the weighted pass: the largest of 64 / 32 / 16 / 8 samples whose LDS fits 64 KB
+static int wmu_tile(int F, int KP) {
+  for (int ts = 64; ts >= 8; ts >>= 1) {
+    const size_t lds = ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
+    if (lds <= 64 * 1024) return ts;
+  }
+  return 0;
+}
+static size_t wmu_lds(int F, int KP, int ts) {
+  return ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
+}
+static constexpr int64_t kWmuMaxBlocks = 1024;
+
 extern "C" {
 
 int cnmf_abi_version(void) { return 201; }
@@ -3863,4 +4074,50 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
   return CNMF_OK;
 }
 
+
+// ---- weighted / masked MU
+int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k) {
+  if (n_rows < 0 || n_features < 1 || n_features > 512 || k < 1 || k > 8)
+    return set_err(CNMF_ERR_UNSUPPORTED, "weighted MU: n_features=%d (1..512), k=%d (1..8)", n_features, k);
+  const int ts = wmu_tile(n_features, k <= 4 ? 4 : 8);
+  if (ts == 0) return set_err(CNMF_ERR_UNSUPPORTED, "weighted MU: no tile fits");
+  const int64_t n_tiles = (n_rows + ts - 1) / ts;
+  return std::min<int64_t>(n_tiles, kWmuMaxBlocks);
+}
+
+int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double* H64, double* partials,
+                         int64_t n_parts, int64_t n_rows, int n_features, int k, int flags, void* stream) {
+  const int64_t G = cnmf_wmu_pass_blocks(n_rows, n_features, k);
+  if (G < 0) return (int)G;
+  if (!X || !M || !W || !H64 || (G > 0 && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  const int valid = CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE | CNMF_PASS_LOSS;
+  if ((flags & ~valid) || flags == 0 || ((flags & CNMF_PASS_LOSS) && flags != CNMF_PASS_LOSS))
+    return set_err(CNMF_ERR_ARG, "invalid flags %d", flags);
+  if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the pass needs %lld",
+                                  (long long)n_parts, (long long)G);
+  if (G == 0) return CNMF_OK;
+  const int KP = k <= 4 ? 4 : 8;
+  const int ts = wmu_tile(n_features, KP);
+  const int64_t n_tiles = (n_rows + ts - 1) / ts;
+  const size_t lds = wmu_lds(n_features, KP, ts);
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  const bool two = n_features > NT;
+  using Fn = void (*)(const float*, const float*, float*, const double*, double*, int64_t, int, int, int, int, int64_t);
+  Fn fn = KP == 4 ? (two ? &wmu_pass_kernel<4, 2> : &wmu_pass_kernel<4, 1>)
+                  : (two ? &wmu_pass_kernel<8, 2> : &wmu_pass_kernel<8, 1>);
+  hipLaunchKernelGGL(fn, dim3((unsigned)G), dim3(NT), lds, hs, X, M, W, H64, partials, n_rows, n_features, k, ts,
+                     flags, n_tiles);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, void* stream) {
+  if (!AD || !H64) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_features < 1 || k < 1) return set_err(CNMF_ERR_SHAPE, "invalid shape F=%d k=%d", n_features, k);
+  const int kF = k * n_features;
+  hipLaunchKernelGGL(wmu_basis_kernel, dim3((unsigned)std::min(64, (kF + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), AD, H64, kF);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
 }  // extern "C"

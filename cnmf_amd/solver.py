@@ -434,3 +434,104 @@ class ALSPlan(MUPlan):
             self.reduce(self.n_out, self.AB)
             self._allreduce(self.AB)
             self.h_step()
+
+
+class WeightedMUPlan:
+    """Device state of the weighted / masked MU (spec: oracle/wmu_ref.py).
+
+    Per iteration: one pass over X and the weights M (`cnmf_wmu_sample_pass`: the W-step and the
+    per-workgroup fp64 rows [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))]), the deterministic fp64 reduction, (multi-GPU:
+    one all_reduce of the 2kF accumulators,) and the H-step (`cnmf_wmu_basis_update`).  The same
+    driver (`run_mu`) runs it: W then H, the weighted error every 10 iterations when tol > 0."""
+
+    persistent = persistent_shape = exchange = False
+
+    def __init__(self, X: torch.Tensor, M: torch.Tensor, n_components: int, group=None):
+        self.lib = _lib.load()
+        if X.dtype != torch.float32 or M.dtype != torch.float32:
+            raise TypeError("weighted MU takes float32 X and weights")
+        if X.shape != M.shape or X.dim() != 2:
+            raise ValueError(f"weights must have X's shape {tuple(X.shape)}, got {tuple(M.shape)}")
+        if X.device.type != "cuda" or M.device.type != "cuda":
+            raise _lib.HipLibraryError("WeightedMUPlan needs X and the weights in HIP device memory")
+        self.X, self.M = X.contiguous(), M.contiguous()
+        self.device = X.device
+        self.n_rows, self.F = map(int, X.shape)
+        self.k = int(n_components)
+        self.tc = torch.float32
+        self.group = group
+        self.world = 1
+        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            self.world = torch.distributed.get_world_size(group)
+        with torch.cuda.device(self.device):
+            nb = self.lib.cnmf_wmu_pass_blocks(self.n_rows, self.F, self.k)
+        check(nb, "cnmf_wmu_pass_blocks")
+        self.n_parts = int(nb)
+        self.n_out = 2 * self.k * self.F
+        dev, f64 = self.device, torch.float64
+        self.W = torch.empty((self.n_rows, self.k), dtype=torch.float32, device=dev)
+        self.H64 = torch.zeros((self.k, self.F), dtype=f64, device=dev)
+        self.partials = torch.zeros((max(self.n_parts, 1), self.n_out), dtype=f64, device=dev)
+        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out)), dtype=f64, device=dev)
+        self.counter = torch.zeros(int(self.lib.cnmf_counter_words()), dtype=torch.int32, device=dev)
+        self.AD = torch.zeros(self.n_out, dtype=f64, device=dev)
+        self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def set_W(self, W):
+        self.W.copy_(torch.as_tensor(W).to(device=self.device, dtype=torch.float32))
+
+    def set_H(self, H):
+        self.H64.copy_(torch.as_tensor(H).to(device=self.device, dtype=torch.float64))
+
+    def H(self, dtype=None) -> torch.Tensor:
+        return self.H64.to(dtype or self.tc)
+
+    def sample_pass(self, flags: int):
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_wmu_sample_pass(
+                _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64), _ptr(self.partials),
+                self.n_parts, self.n_rows, self.F, self.k, flags, self._stream()), "cnmf_wmu_sample_pass")
+
+    def reduce(self, n_out: int, out: torch.Tensor):
+        if self.n_parts == 0:  # an empty shard contributes zeros to the all_reduce
+            out.zero_()
+            return
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_reduce_partials(_ptr(self.partials), self.n_parts, n_out,
+                                                _ptr(self.stage), _ptr(self.counter), _ptr(out),
+                                                self._stream()), "cnmf_reduce_partials")
+
+    def _allreduce(self, t: torch.Tensor):
+        if self.world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+
+    def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
+        """n_iter weighted MU iterations; pass_events: 2·n_iter events recorded around each pass."""
+        ev = list(pass_events) if pass_events is not None else None
+        stream = torch.cuda.current_stream(self.device) if ev is not None else None
+        for i in range(max(n_iter, 0)):
+            if ev is not None:
+                ev[2 * i].record(stream)
+            self.sample_pass(_lib.PASS_UPDATE_W | (_lib.PASS_ACCUMULATE if update_H else 0))
+            if ev is not None:
+                ev[2 * i + 1].record(stream)
+            if not update_H:
+                continue
+            self.reduce(self.n_out, self.AD)
+            self._allreduce(self.AD)
+            with torch.cuda.device(self.device):
+                check(self.lib.cnmf_wmu_basis_update(_ptr(self.AD), _ptr(self.H64), self.F, self.k,
+                                                     self._stream()), "cnmf_wmu_basis_update")
+
+    def check_sync_error(self):
+        pass  # no in-launch waits in the weighted path
+
+    def frobenius_error(self) -> float:
+        """sqrt(Σ m·(x − w·h)²) over all ranks; synchronises."""
+        self.sample_pass(_lib.PASS_LOSS)
+        self.reduce(1, self.loss_buf)
+        self._allreduce(self.loss_buf)
+        return math.sqrt(max(float(self.loss_buf.item()), 0.0))

@@ -209,6 +209,21 @@ int cnmf_als_basis_update(const double* AB, double* H64, double* Ht, double* HHt
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);
 
+/* ---- weighted / masked MU (oracle/wmu_ref.py).  Per-element weights
+ * M >= 0 (N x F fp32, same layout as X; 0 = missing):
+ *   W <- W o ((M o X) H^T) / ((M o (W H)) H^T),   H <- H o (W'^T (M o X)) / (W'^T (M o (W' H)))
+ * (SK:831-870 order and zero-denominator rule SK:620 / SK:706; with M = 1 exactly SK's Frobenius
+ * MU, SK:526-728).  No reference interface: the reference's MU has no weights.  fp32 X / M / W,
+ * H64 the fp64 master basis (k x F); 1 <= k <= 8, 1 <= F <= 512.
+ * cnmf_wmu_pass_blocks: partial rows of one pass (size `partials` as that x 2kF doubles; x 1 for
+ * the loss).  cnmf_wmu_sample_pass flags: UPDATE_W | ACCUMULATE (each workgroup's fp64 row
+ * [W'^T(MoX) | W'^T(Mo(W'H))]) or LOSS alone (each row: sum m (x - wh)^2).  Reduce the rows with
+ * cnmf_reduce_partials (n_out = 2kF, or 1), then cnmf_wmu_basis_update(AD) applies the H-step. */
+int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k);
+int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double* H64, double* partials,
+                         int64_t n_parts, int64_t n_rows, int n_features, int k, int flags, void* stream);
+int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,90 @@
+"""GPU parity of the weighted / masked MU (cnmf_wmu_sample_pass + reduction + cnmf_wmu_basis_update;
+SURVEY.md §8(f) row 2) against the fp64 oracle (oracle/wmu_ref.py) on the same fp32 inputs.
+
+Bar: 1e-5 relative Frobenius on W and H (north_star).  Shapes cover the tile sizes of the pass
+(F = 81: 64-sample tiles; F = 300: 16-sample tiles and two features per thread in phase 2; F = 17
+with k = 3), ragged row counts, masks with 30 % missing entries, unit weights against sklearn's
+golden (cfg1), the tol stop through the API, and the weighted loss.
+"""
+import numpy as np
+import pytest
+
+from golden_io import load, rel_fro
+from oracle import wmu_ref
+
+pytestmark = pytest.mark.gpu
+
+TOL32 = 1e-5
+
+
+def _weights(X, seed, p_missing=0.3):
+    rng = np.random.default_rng(seed)
+    return (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= p_missing)).astype(np.float32)
+
+
+def _plan(X, M, W0, H0):
+    import torch
+    from cnmf_amd.solver import WeightedMUPlan
+    plan = WeightedMUPlan(torch.from_numpy(X).cuda(), torch.from_numpy(M).cuda(), W0.shape[1])
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    return plan
+
+
+def test_unit_weights_match_sklearn_golden():
+    case = load("cfg1_float32")
+    X = case["X"]
+    plan = _plan(X, np.ones_like(X), case["W0"], case["H0"])
+    plan.iterate(200)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = wmu_ref.wmu_fit(X.astype(np.float64), np.ones(X.shape), case["W0"].astype(np.float64),
+                                case["H0"].astype(np.float64), max_iter=200, tol=0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+    # and sklearn's own fp32 run (its fp32 arithmetic differs in the last bits)
+    assert rel_fro(W, case["W"]) <= 1e-4 and rel_fro(H, case["H"]) <= 1e-4
+
+
+@pytest.mark.parametrize("n,F,k", [(5000, 81, 4), (4099, 81, 4), (3001, 300, 8), (777, 17, 3), (64, 81, 1)])
+def test_masked_matches_oracle(n, F, k):
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(n, F, seed=n, dtype=np.float32)
+    M = _weights(X, n)
+    W0, H0 = random_init(X, k, 7)
+    plan = _plan(X, M, W0, H0)
+    n_it = 100
+    plan.iterate(n_it)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                H0.astype(np.float64), max_iter=n_it, tol=0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+    err = plan.frobenius_error()
+    ref = wmu_ref.weighted_error(X.astype(np.float64), M.astype(np.float64), W.astype(np.float64), H)
+    assert abs(err - ref) <= 1e-7 * ref  # the pass multiplies with the fp32-rounded basis
+
+
+def test_tol_stop_through_api():
+    import cnmf_amd
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(2000, 81, seed=4, dtype=np.float32)
+    M = _weights(X, 4)
+    W0, H0 = random_init(X, 4, 42)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom", tol=1e-3,
+                                 max_iter=400, weights=M)
+    Wr, Hr, nr = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                 H0.astype(np.float64), max_iter=400, tol=1e-3)
+    assert n == nr
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32
+    est = cnmf_amd.NMF(4, init="custom", tol=1e-3, max_iter=400)
+    W2 = est.fit_transform(X, W=W0.copy(), H=H0.copy(), weights=M)
+    assert est.n_iter_ == nr and rel_fro(W2, Wr) <= TOL32
+    assert abs(est.reconstruction_err_ - wmu_ref.weighted_error(
+        X.astype(np.float64), M.astype(np.float64), W2.astype(np.float64),
+        est.components_.astype(np.float64))) <= 1e-6 * est.reconstruction_err_
+
+
+def test_native_library_used():
+    """The weighted path is the HIP library's (no CPU fallback exists)."""
+    from cnmf_amd import _lib
+    lib = _lib.load()
+    assert lib.cnmf_wmu_pass_blocks(1000, 81, 4) > 0
+    assert lib.cnmf_wmu_pass_blocks(1000, 600, 4) < 0  # F > 512: refused, not emulated

@@ -3159,6 +3159,7 @@ using namespace cnmf;
 // in fixed order and cnmf_wmu_basis_update applies the H-step.  Loss pass: Σ m·(x − w·h)² in fp64.
 // Limits: k <= 8, F <= 512 (registers of phase 2: NFT features per thread).
 // ------------------------------------------------------------------------------------------------
+constexpr int WMU_MAXC = 8;  // 16-byte chunks per thread and array of one tile (ts·F <= 8192)
 template <int KP, int NFT>
 __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ X, const float* __restrict__ M,
                                                       float* __restrict__ W, const double* __restrict__ H64,
@@ -3167,8 +3168,8 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);  // [ts][F]
   float* sM = sX + ts * F;                     // [ts][F]
-  float* sH = sM + ts * F;                     // [KP][F] (rows >= k zero)
-  float* sWn = sH + KP * F;                    // [ts][KP] the tile's new W
+  float* sHt = sM + ts * F;                    // [F][KP] (columns >= k zero)
+  float* sWn = sHt + KP * F;                   // [ts][KP] the tile's new W
   double* sRed = reinterpret_cast<double*>(smem + ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16);
   const int t = threadIdx.x;
   const int lane = t & 63;
@@ -3178,33 +3179,68 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
   const int P = NT / ts;  // lanes per sample in phase 1 (a power of two <= 64)
   const int sp = t / P;
   const int part = t - sp * P;
-  for (int e = t; e < KP * F; e += NT) sH[e] = e < k * F ? (float)H64[e] : 0.f;
+  for (int e = t; e < KP * F; e += NT) {
+    const int f = e / KP, j = e - f * KP;
+    sHt[e] = j < k ? (float)H64[j * F + f] : 0.f;
+  }
   __syncthreads();
+  // phase-2 threads: F <= 256: G2 = 256/F groups of F threads, group g takes the samples g, g+G2, ..;
+  // F > 256: one group, features t and t + 256.  Each group writes its own fp64 row.
+  const int G2 = NFT == 1 ? NT / F : 1;
+  const int g2 = NFT == 1 ? t / F : 0;
+  const int fb = NFT == 1 ? t - g2 * F : t;
   float hf[NFT][KP];
   double A64[NFT][KP], D64[NFT][KP];
 #pragma unroll
   for (int u = 0; u < NFT; ++u) {
-    const int f = t + NT * u;
+    const int f = fb + NT * u;
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      hf[u][j] = f < F ? sH[j * F + f] : 0.f;
+      hf[u][j] = (g2 < G2 && f < F) ? sHt[f * KP + j] : 0.f;
       A64[u][j] = 0.0;
       D64[u][j] = 0.0;
     }
   }
   double loss = 0.0;
+  // the next tile's X and M ride in registers (16-byte loads of the tile's contiguous span) while
+  // this tile computes; a span whose length is not a multiple of 16 bytes (only a ragged last
+  // tile) stages its tail with 4-byte loads
+  u32x4 px[WMU_MAXC], pm[WMU_MAXC];
+  auto load_tile = [&](int64_t tile) {
+    const int64_t r0 = tile * ts;
+    const int nch = (int)(min<int64_t>(ts, n_rows - r0) * F / 4);
+    const u32x4* x4 = reinterpret_cast<const u32x4*>(X + r0 * F);
+    const u32x4* m4 = reinterpret_cast<const u32x4*>(M + r0 * F);
+#pragma unroll
+    for (int c = 0; c < WMU_MAXC; ++c) {
+      const int i = t + NT * c;
+      if (i < nch) {
+        px[c] = __builtin_nontemporal_load(x4 + i);
+        pm[c] = __builtin_nontemporal_load(m4 + i);
+      }
+    }
+  };
+  if ((int64_t)blockIdx.x < n_tiles) load_tile(blockIdx.x);
   for (int64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     const int64_t r0 = tile * ts;
     const int ns = (int)min<int64_t>(ts, n_rows - r0);
     __syncthreads();  // the previous tile's phase 2 is done with sX / sM / sWn
     {
-      const float* xs = X + r0 * F;
-      const float* ms = M + r0 * F;
-      for (int e = t; e < ns * F; e += NT) {  // the tile's rows are one contiguous span
-        sX[e] = xs[e];
-        sM[e] = ms[e];
+      const int nch = ns * F / 4;
+#pragma unroll
+      for (int c = 0; c < WMU_MAXC; ++c) {
+        const int i = t + NT * c;
+        if (i < nch) {
+          reinterpret_cast<u32x4*>(sX)[i] = px[c];
+          reinterpret_cast<u32x4*>(sM)[i] = pm[c];
+        }
+      }
+      for (int e = 4 * nch + t; e < ns * F; e += NT) {
+        sX[e] = X[r0 * F + e];
+        sM[e] = M[r0 * F + e];
       }
     }
+    if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);
     __syncthreads();
     // ---- phase 1
     {
@@ -3221,9 +3257,18 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
         for (int f = part; f < F; f += P) {
           const double x = (double)xr[f];
           const double m = (double)mr[f];
+          double h[KP];
+#pragma unroll
+          for (int j = 0; j < KP; j += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(sHt + f * KP + j);
+            h[j] = v.x;
+            h[j + 1] = v.y;
+            h[j + 2] = v.z;
+            h[j + 3] = v.w;
+          }
           double rec = 0.0;
 #pragma unroll
-          for (int j = 0; j < KP; ++j) rec = fma(w[j], (double)sH[j * F + f], rec);
+          for (int j = 0; j < KP; ++j) rec = fma(w[j], h[j], rec);
           if (do_loss) {
             const double r = x - rec;
             l = fma(m * r, r, l);
@@ -3231,9 +3276,8 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
             const double mx = m * x, mrec = m * rec;
 #pragma unroll
             for (int j = 0; j < KP; ++j) {
-              const double h = (double)sH[j * F + f];
-              num[j] = fma(mx, h, num[j]);
-              den[j] = fma(mrec, h, den[j]);
+              num[j] = fma(mx, h[j], num[j]);
+              den[j] = fma(mrec, h[j], den[j]);
             }
           }
         }
@@ -3271,12 +3315,12 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
     // ---- phase 2
 #pragma unroll
     for (int u = 0; u < NFT; ++u) {
-      const int f = t + NT * u;
-      if (f < F) {
+      const int f = fb + NT * u;
+      if (g2 < G2 && f < F) {
         float a32[KP], d32[KP];
 #pragma unroll
         for (int j = 0; j < KP; ++j) a32[j] = d32[j] = 0.f;
-        for (int s2 = 0; s2 < ns; ++s2) {
+        for (int s2 = g2; s2 < ns; s2 += G2) {
           const float x = sX[s2 * F + f];
           const float m = sM[s2 * F + f];
           float wr[KP];
@@ -3310,14 +3354,14 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
     for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
     if (lane == 0) sRed[t >> 6] = loss;
     __syncthreads();
-    if (t == 0) partials[blockIdx.x] = (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]);
+    if (t < G2) partials[(size_t)blockIdx.x * G2 + t] = t == 0 ? (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]) : 0.0;
     return;
   }
-  if (!do_acc) return;
-  double* prow = partials + (size_t)blockIdx.x * (2 * k * F);
+  if (!do_acc || g2 >= G2) return;
+  double* prow = partials + ((size_t)blockIdx.x * G2 + g2) * (2 * k * F);
 #pragma unroll
   for (int u = 0; u < NFT; ++u) {
-    const int f = t + NT * u;
+    const int f = fb + NT * u;
     if (f < F)
 #pragma unroll
       for (int j = 0; j < KP; ++j)
@@ -3341,14 +3385,15 @@ __global__ __launch_bounds__(256) void wmu_basis_kernel(const double* __restrict
 static int wmu_tile(int F, int KP) {
   for (int ts = 64; ts >= 8; ts >>= 1) {
     const size_t lds = ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
-    if (lds <= 64 * 1024) return ts;
+    if (lds <= 64 * 1024 && ts * F <= 4 * NT * WMU_MAXC) return ts;
   }
   return 0;
 }
 static size_t wmu_lds(int F, int KP, int ts) {
   return ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
 }
-static constexpr int64_t kWmuMaxBlocks = 1024;
+static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy 2 waves / SIMD)
+static int wmu_groups(int F) { return F <= NT ? NT / F : 1; }  // partial rows per workgroup
 
 extern "C" {
 
@@ -4082,7 +4127,7 @@ int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k) {
   const int ts = wmu_tile(n_features, k <= 4 ? 4 : 8);
   if (ts == 0) return set_err(CNMF_ERR_UNSUPPORTED, "weighted MU: no tile fits");
   const int64_t n_tiles = (n_rows + ts - 1) / ts;
-  return std::min<int64_t>(n_tiles, kWmuMaxBlocks);
+  return std::min<int64_t>(n_tiles, kWmuMaxBlocks) * wmu_groups(n_features);  // partial rows
 }
 
 int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double* H64, double* partials,
@@ -4090,12 +4135,15 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
   const int64_t G = cnmf_wmu_pass_blocks(n_rows, n_features, k);
   if (G < 0) return (int)G;
   if (!X || !M || !W || !H64 || (G > 0 && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(M) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and the weights must be 16-byte aligned");
   const int valid = CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE | CNMF_PASS_LOSS;
   if ((flags & ~valid) || flags == 0 || ((flags & CNMF_PASS_LOSS) && flags != CNMF_PASS_LOSS))
     return set_err(CNMF_ERR_ARG, "invalid flags %d", flags);
   if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the pass needs %lld",
                                   (long long)n_parts, (long long)G);
   if (G == 0) return CNMF_OK;
+  const int64_t grid = G / wmu_groups(n_features);
   const int KP = k <= 4 ? 4 : 8;
   const int ts = wmu_tile(n_features, KP);
   const int64_t n_tiles = (n_rows + ts - 1) / ts;
@@ -4105,7 +4153,7 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
   using Fn = void (*)(const float*, const float*, float*, const double*, double*, int64_t, int, int, int, int, int64_t);
   Fn fn = KP == 4 ? (two ? &wmu_pass_kernel<4, 2> : &wmu_pass_kernel<4, 1>)
                   : (two ? &wmu_pass_kernel<8, 2> : &wmu_pass_kernel<8, 1>);
-  hipLaunchKernelGGL(fn, dim3((unsigned)G), dim3(NT), lds, hs, X, M, W, H64, partials, n_rows, n_features, k, ts,
+  hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(NT), lds, hs, X, M, W, H64, partials, n_rows, n_features, k, ts,
                      flags, n_tiles);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;

@@ -3159,6 +3159,7 @@ using namespace cnmf;
 // in fixed order and cnmf_wmu_basis_update applies the H-step.  Loss pass: Σ m·(x − w·h)² in fp64.
 // Limits: k <= 8, F <= 512 (registers of phase 2: NFT features per thread).
 // ------------------------------------------------------------------------------------------------
+constexpr int WMU_CH = 5;    // features per fp32 chain in phase 1
 constexpr int WMU_MAXC = 8;  // 16-byte chunks per thread and array of one tile (ts·F <= 8192)
 template <int KP, int NFT>
 __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ X, const float* __restrict__ M,
@@ -3170,7 +3171,8 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
   float* sM = sX + ts * F;                     // [ts][F]
   float* sHt = sM + ts * F;                    // [F][KP] (columns >= k zero)
   float* sWn = sHt + KP * F;                   // [ts][KP] the tile's new W
-  double* sRed = reinterpret_cast<double*>(smem + ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16);
+  float* sW = sWn + ts * KP;                   // [ts][k] the tile's W (staged with X and M)
+  double* sRed = reinterpret_cast<double*>(smem + ((size_t)(2 * ts * F + KP * F + 2 * ts * KP) * 4 + 15) / 16 * 16);
   const int t = threadIdx.x;
   const int lane = t & 63;
   const bool do_loss = (flags & CNMF_PASS_LOSS) != 0;
@@ -3205,12 +3207,14 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
   // the next tile's X and M ride in registers (16-byte loads of the tile's contiguous span) while
   // this tile computes; a span whose length is not a multiple of 16 bytes (only a ragged last
   // tile) stages its tail with 4-byte loads
-  u32x4 px[WMU_MAXC], pm[WMU_MAXC];
+  u32x4 px[WMU_MAXC], pm[WMU_MAXC], pw;
   auto load_tile = [&](int64_t tile) {
     const int64_t r0 = tile * ts;
-    const int nch = (int)(min<int64_t>(ts, n_rows - r0) * F / 4);
+    const int nsr = (int)min<int64_t>(ts, n_rows - r0);
+    const int nch = nsr * F / 4;
     const u32x4* x4 = reinterpret_cast<const u32x4*>(X + r0 * F);
     const u32x4* m4 = reinterpret_cast<const u32x4*>(M + r0 * F);
+    if (t < nsr * k / 4) pw = reinterpret_cast<const u32x4*>(W + r0 * k)[t];  // the tile's W span
 #pragma unroll
     for (int c = 0; c < WMU_MAXC; ++c) {
       const int i = t + NT * c;
@@ -3239,6 +3243,8 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
         sX[e] = X[r0 * F + e];
         sM[e] = M[r0 * F + e];
       }
+      if (t < ns * k / 4) reinterpret_cast<u32x4*>(sW)[t] = pw;
+      for (int e = ns * k / 4 * 4 + t; e < ns * k; e += NT) sW[e] = W[r0 * k + e];
     }
     if (tile + gridDim.x < n_tiles) load_tile(tile + gridDim.x);
     __syncthreads();
@@ -3247,37 +3253,59 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
       const bool valid = sp < ns;
       double w[KP];
 #pragma unroll
-      for (int j = 0; j < KP; ++j) w[j] = (valid && j < k) ? (double)W[(r0 + sp) * k + j] : 0.0;
+      for (int j = 0; j < KP; ++j) w[j] = (valid && j < k) ? (double)sW[sp * k + j] : 0.0;
       double num[KP], den[KP], l = 0.0;
 #pragma unroll
       for (int j = 0; j < KP; ++j) num[j] = den[j] = 0.0;
       if (valid) {
         const float* xr = sX + sp * F;
         const float* mr = sM + sp * F;
-        for (int f = part; f < F; f += P) {
-          const double x = (double)xr[f];
-          const double m = (double)mr[f];
-          double h[KP];
+        if (do_loss) {
+          for (int f = part; f < F; f += P) {
+            double rec = 0.0;
 #pragma unroll
-          for (int j = 0; j < KP; j += 4) {
-            const float4 v = *reinterpret_cast<const float4*>(sHt + f * KP + j);
-            h[j] = v.x;
-            h[j + 1] = v.y;
-            h[j + 2] = v.z;
-            h[j + 3] = v.w;
+            for (int j = 0; j < KP; ++j) rec = fma(w[j], (double)sHt[f * KP + j], rec);
+            const double r = (double)xr[f] - rec;
+            l = fma((double)mr[f] * r, r, l);
           }
-          double rec = 0.0;
+        } else {
+          // fp32 chains of WMU_CH features folded into fp64 (the precision note of phase12)
+          float w32[KP];
 #pragma unroll
-          for (int j = 0; j < KP; ++j) rec = fma(w[j], h[j], rec);
-          if (do_loss) {
-            const double r = x - rec;
-            l = fma(m * r, r, l);
-          } else {
-            const double mx = m * x, mrec = m * rec;
+          for (int j = 0; j < KP; ++j) w32[j] = (float)w[j];
+          for (int f0 = part; f0 < F; f0 += WMU_CH * P) {
+            float nc[KP], dc[KP];
+#pragma unroll
+            for (int j = 0; j < KP; ++j) nc[j] = dc[j] = 0.f;
+#pragma unroll
+            for (int c = 0; c < WMU_CH; ++c) {
+              const int f = f0 + c * P;
+              if (f < F) {
+                float h[KP];
+#pragma unroll
+                for (int j = 0; j < KP; j += 4) {
+                  const float4 v = *reinterpret_cast<const float4*>(sHt + f * KP + j);
+                  h[j] = v.x;
+                  h[j + 1] = v.y;
+                  h[j + 2] = v.z;
+                  h[j + 3] = v.w;
+                }
+                float rec = 0.f;
+#pragma unroll
+                for (int j = 0; j < KP; ++j) rec = fmaf(w32[j], h[j], rec);
+                const float m = mr[f];
+                const float mx = m * xr[f], mrec = m * rec;
+#pragma unroll
+                for (int j = 0; j < KP; ++j) {
+                  nc[j] = fmaf(mx, h[j], nc[j]);
+                  dc[j] = fmaf(mrec, h[j], dc[j]);
+                }
+              }
+            }
 #pragma unroll
             for (int j = 0; j < KP; ++j) {
-              num[j] = fma(mx, h[j], num[j]);
-              den[j] = fma(mrec, h[j], den[j]);
+              num[j] += (double)nc[j];
+              den[j] += (double)dc[j];
             }
           }
         }
@@ -3320,6 +3348,7 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
         float a32[KP], d32[KP];
 #pragma unroll
         for (int j = 0; j < KP; ++j) a32[j] = d32[j] = 0.f;
+#pragma unroll 4
         for (int s2 = g2; s2 < ns; s2 += G2) {
           const float x = sX[s2 * F + f];
           const float m = sM[s2 * F + f];
@@ -3384,13 +3413,13 @@ __global__ __launch_bounds__(256) void wmu_basis_kernel(const double* __restrict
 // tile size of the weighted pass: the largest of 64 / 32 / 16 / 8 samples whose LDS fits 64 KB
 static int wmu_tile(int F, int KP) {
   for (int ts = 64; ts >= 8; ts >>= 1) {
-    const size_t lds = ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
+    const size_t lds = ((size_t)(2 * ts * F + KP * F + 2 * ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
     if (lds <= 64 * 1024 && ts * F <= 4 * NT * WMU_MAXC) return ts;
   }
   return 0;
 }
 static size_t wmu_lds(int F, int KP, int ts) {
-  return ((size_t)(2 * ts * F + KP * F + ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
+  return ((size_t)(2 * ts * F + KP * F + 2 * ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
 }
 static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy 2 waves / SIMD)
 static int wmu_groups(int F) { return F <= NT ? NT / F : 1; }  // partial rows per workgroup
@@ -4135,8 +4164,9 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
   const int64_t G = cnmf_wmu_pass_blocks(n_rows, n_features, k);
   if (G < 0) return (int)G;
   if (!X || !M || !W || !H64 || (G > 0 && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
-  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(M) & 15))
-    return set_err(CNMF_ERR_ALIGN, "X and the weights must be 16-byte aligned");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(M) & 15) ||
+      (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X, the weights and W must be 16-byte aligned");
   const int valid = CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE | CNMF_PASS_LOSS;
   if ((flags & ~valid) || flags == 0 || ((flags & CNMF_PASS_LOSS) && flags != CNMF_PASS_LOSS))
     return set_err(CNMF_ERR_ARG, "invalid flags %d", flags);

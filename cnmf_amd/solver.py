@@ -522,9 +522,13 @@ class WeightedMUPlan:
                 continue
             self.reduce(self.n_out, self.AD)
             self._allreduce(self.AD)
-            with torch.cuda.device(self.device):
-                check(self.lib.cnmf_wmu_basis_update(_ptr(self.AD), _ptr(self.H64), self.F, self.k,
-                                                     self._stream()), "cnmf_wmu_basis_update")
+            self.basis_update()
+
+    def basis_update(self):
+        """H <- H ∘ A / D from the (all-reduced) accumulators AD = [A | D]."""
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_wmu_basis_update(_ptr(self.AD), _ptr(self.H64), self.F, self.k,
+                                                 self._stream()), "cnmf_wmu_basis_update")
 
     def check_sync_error(self):
         pass  # no in-launch waits in the weighted path

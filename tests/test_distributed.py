@@ -17,8 +17,8 @@ import torch.multiprocessing as mp
 
 from cnmf_amd import _lib
 from cnmf_amd.distributed import shard_bounds
-from cnmf_amd.solver import MUPlan, run_mu
-from oracle import mu_ref
+from cnmf_amd.solver import MUPlan, WeightedMUPlan, run_mu
+from oracle import mu_ref, wmu_ref
 
 
 class _NumpyPlan(MUPlan):
@@ -101,6 +101,79 @@ def test_two_rank_gloo_matches_unsharded(tol, max_iter):
     out = manager.dict()
     mp.spawn(_worker, args=(2, _free_port(), X, W0, H0, max_iter, tol, out), nprocs=2, join=True)
     Wr, Hr, nr = mu_ref.mu_fit(X, W0, H0, max_iter=max_iter, tol=tol)
+    W = np.zeros_like(W0)
+    for rank in range(2):
+        lo, hi, Wp, Hp, n_iter = out[rank]
+        W[lo:hi] = Wp
+        assert n_iter == nr
+        np.testing.assert_allclose(Hp, Hr, rtol=1e-10, atol=1e-14)
+    np.testing.assert_allclose(W, Wr, rtol=1e-10, atol=1e-14)
+
+
+class _NumpyWeightedPlan(WeightedMUPlan):
+    """WeightedMUPlan with its launches done by the weighted oracle on CPU (fp64)."""
+
+    def __init__(self, X, M, W, H, group=None):  # noqa: D107 — no super(): no HIP buffers
+        self.X = np.asarray(X, dtype=np.float64)
+        self.Mw = np.asarray(M, dtype=np.float64)
+        self.n_rows, self.F = self.X.shape
+        self.k = H.shape[0]
+        self.n_out = 2 * self.k * self.F
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.Wn = np.array(W, dtype=np.float64)
+        self.Hn = np.array(H, dtype=np.float64)
+        self.AD = torch.zeros(self.n_out, dtype=torch.float64)
+        self.loss_buf = torch.zeros(1, dtype=torch.float64)
+        self._partial = None
+
+    def sample_pass(self, flags):
+        if flags & _lib.PASS_LOSS:
+            R = self.X - self.Wn @ self.Hn
+            self._partial = np.array([np.sum(self.Mw * R * R)])
+            return
+        self.Wn = wmu_ref.update_w(self.X, self.Mw, self.Wn, self.Hn)
+        if flags & _lib.PASS_ACCUMULATE:
+            A = self.Wn.T @ (self.Mw * self.X)
+            D = self.Wn.T @ (self.Mw * (self.Wn @ self.Hn))
+            self._partial = np.concatenate([A.ravel(), D.ravel()])
+
+    def reduce(self, n_out, out):
+        out.copy_(torch.from_numpy(self._partial[:n_out]))
+
+    def basis_update(self):
+        AD = self.AD.numpy()
+        kF = self.k * self.F
+        A, D = AD[:kF].reshape(self.k, self.F), AD[kF:].reshape(self.k, self.F).copy()
+        D[D == 0] = wmu_ref.EPSILON
+        self.Hn = self.Hn * (A / D)
+
+
+def _wworker(rank, world, port, X, M, W0, H0, max_iter, tol, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_bounds(X.shape[0], world, rank)
+        plan = _NumpyWeightedPlan(X[lo:hi], M[lo:hi], W0[lo:hi], H0)
+        n_iter = run_mu(plan, max_iter=max_iter, tol=tol)
+        out[rank] = (lo, hi, plan.Wn, plan.Hn, n_iter)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tol,max_iter", [(0.0, 30), (1e-3, 400)])
+def test_two_rank_gloo_weighted_matches_unsharded(tol, max_iter):
+    """The weighted MU's host path (WeightedMUPlan.iterate + run_mu at world 2: one all_reduce of the
+    2kF accumulators per iteration, one double per error check) reproduces the unsharded oracle."""
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(301, 81, seed=12, dtype=np.float64)
+    rng = np.random.default_rng(5)
+    M = rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)
+    W0, H0 = random_init(X, 4, 3)
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_wworker, args=(2, _free_port(), X, M, W0, H0, max_iter, tol, out), nprocs=2, join=True)
+    Wr, Hr, nr = wmu_ref.wmu_fit(X, M, W0, H0, max_iter=max_iter, tol=tol)
     W = np.zeros_like(W0)
     for rank in range(2):
         lo, hi, Wp, Hp, n_iter = out[rank]

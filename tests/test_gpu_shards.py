@@ -87,3 +87,47 @@ def test_two_process_shards_match_oracle():
                                max_iter=200, tol=1e-4)
     assert res[0][5] == nr
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def _wworker(rank, world, port, X, M, W0, H0, n_iter, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cnmf_amd.distributed import factorise_sharded, shard_bounds
+        lo, hi = shard_bounds(X.shape[0], world, rank)
+        W, H, n = factorise_sharded(torch.from_numpy(X[lo:hi]), W0[lo:hi], H0, max_iter=n_iter,
+                                    tol=1e-3, weights=M[lo:hi])
+        q.put((rank, lo, hi, W.cpu().numpy(), H.double().cpu().numpy(), n))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_process_weighted_shards_match_oracle():
+    """The weighted / masked MU sharded over 2 processes (factorise_sharded(weights=...))."""
+    import torch.multiprocessing as mp
+    from oracle import wmu_ref
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(3001, 81, seed=8, dtype=np.float32)
+    rng = np.random.default_rng(8)
+    M = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wworker, args=(r, 2, port, X, M, W0, H0, 200, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    res.sort()
+    W = np.concatenate([r[3] for r in res])
+    H = res[0][4]
+    assert np.array_equal(res[0][4], res[1][4]) and res[0][5] == res[1][5]
+    Wr, Hr, nr = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                 H0.astype(np.float64), max_iter=200, tol=1e-3)
+    assert res[0][5] == nr
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))

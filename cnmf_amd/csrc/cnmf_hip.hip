@@ -4156,7 +4156,10 @@ int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k) {
   const int ts = wmu_tile(n_features, k <= 4 ? 4 : 8);
   if (ts == 0) return set_err(CNMF_ERR_UNSUPPORTED, "weighted MU: no tile fits");
   const int64_t n_tiles = (n_rows + ts - 1) / ts;
-  return std::min<int64_t>(n_tiles, kWmuMaxBlocks) * wmu_groups(n_features);  // partial rows
+  const int64_t g2 = wmu_groups(n_features);
+  // partial rows (one per workgroup and phase-2 group), within one reduction's capacity
+  const int64_t max_wg = std::min<int64_t>(kWmuMaxBlocks, (int64_t)NSLICE * 4 * RED_ROWS_PER_THREAD / g2);
+  return std::min<int64_t>(n_tiles, max_wg) * g2;
 }
 
 int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double* H64, double* partials,

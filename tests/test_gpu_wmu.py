@@ -88,3 +88,22 @@ def test_native_library_used():
     lib = _lib.load()
     assert lib.cnmf_wmu_pass_blocks(1000, 81, 4) > 0
     assert lib.cnmf_wmu_pass_blocks(1000, 600, 4) < 0  # F > 512: refused, not emulated
+
+
+def test_fully_masked_rows_and_columns():
+    """A sample with every weight 0 (num = den = 0 -> eps: its w becomes 0) and a feature with every
+    weight 0 (its H column becomes 0), as in the oracle; the rest still matches at 1e-5."""
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1500, 81, seed=21, dtype=np.float32)
+    M = _weights(X, 21)
+    M[[0, 77, 1499], :] = 0.0
+    M[:, [5, 80]] = 0.0
+    W0, H0 = random_init(X, 4, 2)
+    plan = _plan(X, M, W0, H0)
+    plan.iterate(40)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                H0.astype(np.float64), max_iter=40, tol=0)
+    assert np.all(W[[0, 77, 1499]] == 0) and np.all(Wr[[0, 77, 1499]] == 0)
+    assert np.all(H[:, [5, 80]] == 0) and np.all(Hr[:, [5, 80]] == 0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))

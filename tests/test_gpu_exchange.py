@@ -46,14 +46,31 @@ def _plan(X, W0, H0, group=None):
     return plan
 
 
-def test_self_exchange_is_bit_identical():
+@pytest.fixture(params=[1, 2, 3], ids=["pairs", "teams", "floating"])
+def layout(request):
+    """Every persistent layout a rank may pick (MUPlan.tune runs them all at N > 1 too); the
+    multi-GPU launch serves layout 3 with layout 1 (floating tiles are single-GPU only)."""
+    from cnmf_amd import _lib
+    lib = _lib.load()
+    old = lib.cnmf_get_persist_variant()
+    assert lib.cnmf_set_persist_variant(request.param) == 0
+    yield request.param
+    lib.cnmf_set_persist_variant(old)
+
+
+def test_self_exchange_is_bit_identical(layout):
     import torch
     import torch.distributed as dist
+    from cnmf_amd import _lib
     X, W0, H0 = _data(64 * 1500, 5)
+    lib = _lib.load()
+    if layout == 3:  # the multi launch runs layout 1: compare with the single-GPU layout 1
+        lib.cnmf_set_persist_variant(1)
     ref = _plan(X, W0, H0)
     assert ref.persistent
     ref.iterate(25)
     ref.check_sync_error()
+    lib.cnmf_set_persist_variant(layout)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
     try:
         plan = _plan(X, W0, H0)

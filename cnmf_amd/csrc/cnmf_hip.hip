@@ -3165,7 +3165,7 @@ template <int KP, int NFT>
 __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ X, const float* __restrict__ M,
                                                       float* __restrict__ W, const double* __restrict__ H64,
                                                       double* __restrict__ partials, int64_t n_rows, int F,
-                                                      int k, int ts, int flags, int64_t n_tiles) {
+                                                      int k, int ts, int flags, int64_t n_tiles, int rows) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);  // [ts][F]
   float* sM = sX + ts * F;                     // [ts][F]
@@ -3383,10 +3383,30 @@ __global__ __launch_bounds__(NT) void wmu_pass_kernel(const float* __restrict__ 
     for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
     if (lane == 0) sRed[t >> 6] = loss;
     __syncthreads();
-    if (t < G2) partials[(size_t)blockIdx.x * G2 + t] = t == 0 ? (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]) : 0.0;
+    if (t < rows) partials[(size_t)blockIdx.x * rows + t] = t == 0 ? (sRed[0] + sRed[1]) + (sRed[2] + sRed[3]) : 0.0;
     return;
   }
-  if (!do_acc || g2 >= G2) return;
+  if (!do_acc) return;
+  if (rows == 1 && G2 > 1) {  // the G2 groups' sums folded in LDS (fixed order): one row per workgroup
+    __syncthreads();          // every thread is done with the tile's LDS
+    double* sF = reinterpret_cast<double*>(smem);  // [G2][2k][F]
+    if (g2 < G2 && fb < F)
+#pragma unroll
+      for (int j = 0; j < KP; ++j)
+        if (j < k) {
+          sF[(g2 * 2 * k + j) * F + fb] = A64[0][j];
+          sF[(g2 * 2 * k + k + j) * F + fb] = D64[0][j];
+        }
+    __syncthreads();
+    double* prow = partials + (size_t)blockIdx.x * (2 * k * F);
+    for (int e = t; e < 2 * k * F; e += NT) {
+      double v = 0.0;
+      for (int g = 0; g < G2; ++g) v += sF[(size_t)g * 2 * k * F + e];
+      prow[e] = v;
+    }
+    return;
+  }
+  if (g2 >= G2) return;
   double* prow = partials + ((size_t)blockIdx.x * G2 + g2) * (2 * k * F);
 #pragma unroll
   for (int u = 0; u < NFT; ++u) {
@@ -3421,8 +3441,16 @@ static int wmu_tile(int F, int KP) {
 static size_t wmu_lds(int F, int KP, int ts) {
   return ((size_t)(2 * ts * F + KP * F + 2 * ts * KP) * 4 + 15) / 16 * 16 + NWAVE * 8;
 }
+// partial rows per workgroup: 1 when the phase-2 groups' sums fold in the pass's own LDS, else one
+// per group (the reduction then sums them)
+static int wmu_rows(int F, int k) {
+  const int g2 = F <= NT ? NT / F : 1;
+  if (g2 == 1) return 1;
+  const int KP = k <= 4 ? 4 : 8;
+  const int ts = wmu_tile(F, KP);
+  return (size_t)g2 * 2 * k * F * 8 <= wmu_lds(F, KP, ts) ? 1 : g2;
+}
 static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy 2 waves / SIMD)
-static int wmu_groups(int F) { return F <= NT ? NT / F : 1; }  // partial rows per workgroup
 
 extern "C" {
 
@@ -4156,7 +4184,7 @@ int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k) {
   const int ts = wmu_tile(n_features, k <= 4 ? 4 : 8);
   if (ts == 0) return set_err(CNMF_ERR_UNSUPPORTED, "weighted MU: no tile fits");
   const int64_t n_tiles = (n_rows + ts - 1) / ts;
-  const int64_t g2 = wmu_groups(n_features);
+  const int64_t g2 = wmu_rows(n_features, k);
   // partial rows (one per workgroup and phase-2 group), within one reduction's capacity
   const int64_t max_wg = std::min<int64_t>(kWmuMaxBlocks, (int64_t)NSLICE * 4 * RED_ROWS_PER_THREAD / g2);
   return std::min<int64_t>(n_tiles, max_wg) * g2;
@@ -4176,18 +4204,19 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
   if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the pass needs %lld",
                                   (long long)n_parts, (long long)G);
   if (G == 0) return CNMF_OK;
-  const int64_t grid = G / wmu_groups(n_features);
+  const int rows = wmu_rows(n_features, k);
+  const int64_t grid = G / rows;
   const int KP = k <= 4 ? 4 : 8;
   const int ts = wmu_tile(n_features, KP);
   const int64_t n_tiles = (n_rows + ts - 1) / ts;
   const size_t lds = wmu_lds(n_features, KP, ts);
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   const bool two = n_features > NT;
-  using Fn = void (*)(const float*, const float*, float*, const double*, double*, int64_t, int, int, int, int, int64_t);
+  using Fn = void (*)(const float*, const float*, float*, const double*, double*, int64_t, int, int, int, int, int64_t, int);
   Fn fn = KP == 4 ? (two ? &wmu_pass_kernel<4, 2> : &wmu_pass_kernel<4, 1>)
                   : (two ? &wmu_pass_kernel<8, 2> : &wmu_pass_kernel<8, 1>);
   hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(NT), lds, hs, X, M, W, H64, partials, n_rows, n_features, k, ts,
-                     flags, n_tiles);
+                     flags, n_tiles, rows);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }

@@ -206,6 +206,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    group = dist.group.WORLD if dist_path else None
 
     from cnmf_amd.solver import ALSPlan, MUPlan, WeightedMUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
@@ -224,11 +225,11 @@ def main():
     if args.weighted:
         rng = np.random.default_rng(rank)
         Mw = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)
-        plan = WeightedMUPlan(Xd, torch.from_numpy(Mw).to(dev), k)
+        plan = WeightedMUPlan(Xd, torch.from_numpy(Mw).to(dev), k, group=group)
     elif args.solver == "als":
-        plan = ALSPlan(Xd, k, sum_to_one=args.sum_to_one, smoothness=args.smoothness)
+        plan = ALSPlan(Xd, k, sum_to_one=args.sum_to_one, smoothness=args.smoothness, group=group)
     else:
-        plan = MUPlan(Xd, k)
+        plan = MUPlan(Xd, k, group=group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     exchange = None

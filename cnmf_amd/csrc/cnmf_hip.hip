@@ -1130,16 +1130,25 @@ __device__ __forceinline__ float dpp_add(float v) {
 // 16-byte chunk i of this thread for tile `tile`: X chunk (t + 256 i), or for i = 5 and t < 80 the
 // tail of X (t < 16) / the W tile (16 <= t < 80); threads t >= 80 re-read X chunk t (not stored).
 // LOADW = false (W resident in LDS): the W slots re-read X chunk t as well.
+#ifdef CNMF_X_PLAIN  // diagnostic build: default-policy X loads instead of non-temporal ones
+#define SL_XLOAD(p) (*(p))
+#else
+#define SL_XLOAD(p) __builtin_nontemporal_load(p)
+#endif
 template <bool LOADW = true>
 __device__ __forceinline__ void sl_prefetch(u32x4 (&pf)[PFN], const unsigned char* __restrict__ X,
                                             const unsigned char* __restrict__ W, int64_t tile, int t) {
+#ifdef CNMF_DIAG_L2  // diagnostic build: every tile reads one of 64 L2-resident tiles (compute floor)
+  const unsigned char* xs = X + (size_t)(tile & 63) * XB + 16 * t;
+#else
   const unsigned char* xs = X + (size_t)tile * XB + 16 * t;
+#endif
 #pragma unroll
   for (int i = 0; i < PFN - 1; ++i)
-    pf[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xs + 4096 * i));
+    pf[i] = SL_XLOAD(reinterpret_cast<const u32x4*>(xs + 4096 * i));
   const unsigned char* last = t < 16 ? xs + 4096 * (PFN - 1)
                                      : ((LOADW && t < 80) ? W + (size_t)tile * WB + 16 * (t - 16) : xs);
-  pf[PFN - 1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(last));
+  pf[PFN - 1] = SL_XLOAD(reinterpret_cast<const u32x4*>(last));
 }
 
 template <bool STAGEW = true>
@@ -2938,7 +2947,7 @@ __global__ __launch_bounds__(256) void hbm_probe_kernel(const u32x4* __restrict_
   for (; i + 7 * stride < n16; i += 8 * stride) {
     u32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(buf + i + u * stride);
+    for (int u = 0; u < 8; ++u) v[u] = SL_XLOAD(buf + i + u * stride);
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
   }

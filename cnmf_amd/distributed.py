@@ -52,10 +52,11 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     """
     if not (dist.is_available() and dist.is_initialized()):
         raise RuntimeError("factorise_sharded needs an initialised torch.distributed process group")
+    group = group if group is not None else dist.group.WORLD
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     X = torch.as_tensor(X_shard).to(dev).contiguous()
     H0 = torch.as_tensor(H0).to(dev, torch.float64).contiguous()
-    dist.broadcast(H0, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    dist.broadcast(H0, src=dist.get_global_rank(group, 0), group=group)
     if weights is not None:
         if any((l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H)) or exchange:
             raise ValueError("the weighted MU takes no regularisation and no in-launch exchange")

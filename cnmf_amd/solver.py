@@ -30,6 +30,15 @@ def _ptr(t: torch.Tensor | None):
     return None if t is None else t.data_ptr()
 
 
+def plan_world(group) -> int:
+    """Ranks a plan's accumulators are summed over: the size of `group` when one is given, else 1.
+    A plan built without a group is a single-process fit even inside an initialised default group
+    (independent per-rank fits under torchrun, e.g. cNMF replicates, must not all-reduce)."""
+    if group is None:
+        return 1
+    return torch.distributed.get_world_size(group)
+
+
 def _event_array(events):
     if events is None:
         return None, 0
@@ -59,9 +68,7 @@ class MUPlan:
         self.tc = torch.float64 if X.dtype == torch.float64 else torch.float32
         self.l1_W, self.l2_W, self.l1_H, self.l2_H = map(float, (l1_W, l2_W, l1_H, l2_H))
         self.group = group
-        self.world = 1
-        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
-            self.world = torch.distributed.get_world_size(group)
+        self.world = plan_world(group)
         KP = self.lib.cnmf_padded_k(self.k)
         if KP < 0:
             raise _lib.HipLibraryError(f"n_components={self.k} is not supported (1..16)")
@@ -99,8 +106,8 @@ class MUPlan:
         n iterations as ONE launch per rank.  Raises (on every rank) when any rank's shard is not a
         persistent shape or any buffer cannot be shared; the plan then stays on the RCCL path."""
         dist = torch.distributed
-        if self.group is None and not (dist.is_available() and dist.is_initialized()):
-            raise RuntimeError("enable_exchange needs an initialised torch.distributed group")
+        if self.group is None:
+            raise RuntimeError("enable_exchange needs the plan's torch.distributed group (MUPlan(..., group=...))")
         rank = dist.get_rank(self.group)
         ok = torch.tensor([1.0 if self.persistent_shape else 0.0])
         handle, ptr, err = None, ctypes.c_void_p(), ""
@@ -233,8 +240,7 @@ class MUPlan:
                 self.l2_H, int(apply_first), self._stream()), "cnmf_mu_shard_step")
 
     def _allreduce(self, t: torch.Tensor):
-        if self.world > 1 or (self.shard_steps and torch.distributed.is_available()
-                              and torch.distributed.is_initialized()):
+        if self.world > 1 or (self.shard_steps and self.group is not None):
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
     def check_sync_error(self):
@@ -251,6 +257,10 @@ class MUPlan:
                     "the results of that launch are invalid")
             raise _lib.HipLibraryError("persistent MU launch timed out waiting for a workgroup "
                                        "(grid not co-resident?); results of that launch are invalid")
+
+    def counters_at_rest(self) -> bool:
+        """Every ticket, flag, pool and the error word back at zero."""
+        return int(self.counter.cpu().numpy().astype("int64").sum()) == 0
 
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
         """n_iter MU iterations (SK:831-870) without host synchronisation.  pass_events: optional
@@ -460,9 +470,7 @@ class WeightedMUPlan:
         self.k = int(n_components)
         self.tc = torch.float32
         self.group = group
-        self.world = 1
-        if group is not None or (torch.distributed.is_available() and torch.distributed.is_initialized()):
-            self.world = torch.distributed.get_world_size(group)
+        self.world = plan_world(group)
         with torch.cuda.device(self.device):
             nb = self.lib.cnmf_wmu_pass_blocks(self.n_rows, self.F, self.k)
         check(nb, "cnmf_wmu_pass_blocks")

@@ -17,7 +17,7 @@ import torch.multiprocessing as mp
 
 from cnmf_amd import _lib
 from cnmf_amd.distributed import shard_bounds
-from cnmf_amd.solver import MUPlan, WeightedMUPlan, run_mu
+from cnmf_amd.solver import MUPlan, WeightedMUPlan, plan_world, run_mu
 from oracle import mu_ref, wmu_ref
 
 
@@ -32,7 +32,8 @@ class _NumpyPlan(MUPlan):
         self.n_out = self.k * self.V
         self.l1_W, self.l2_W, self.l1_H, self.l2_H = regs
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = plan_world(group)
+        self.shard_steps = False
         self.Wn = np.array(W, dtype=np.float64)
         self.Hn = np.array(H, dtype=np.float64)
         self.AB = torch.zeros(self.n_out, dtype=torch.float64)
@@ -77,11 +78,43 @@ def _worker(rank, world, port, X, W0, H0, max_iter, tol, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lo, hi = shard_bounds(X.shape[0], world, rank)
-        plan = _NumpyPlan(X[lo:hi], W0[lo:hi], H0)
+        plan = _NumpyPlan(X[lo:hi], W0[lo:hi], H0, group=dist.group.WORLD)
         n_iter = run_mu(plan, max_iter=max_iter, tol=tol)
         out[rank] = (lo, hi, plan.Wn, plan.Hn, n_iter)
     finally:
         dist.destroy_process_group()
+
+
+def _indep_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from cnmf_amd.synthetic import iop_spectra, random_init
+        assert plan_world(None) == 1 and plan_world(dist.group.WORLD) == world
+        # an independent fit per rank (cNMF replicates under torchrun): different data on each rank,
+        # no group passed -> nothing may be all-reduced across the ranks
+        X = iop_spectra(200 + 37 * rank, 81, seed=rank, dtype=np.float64)
+        W0, H0 = random_init(X, 4, 5 + rank)
+        plan = _NumpyPlan(X, W0, H0)
+        plan.shard_steps = True  # the shard-step iteration; without a group it all-reduces nothing
+        n_iter = run_mu(plan, max_iter=50, tol=1e-3)
+        out[rank] = (X, W0, H0, plan.Wn, plan.Hn, n_iter)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_plan_without_group_is_a_single_process_fit():
+    """a plan built without a group inside an initialised default group fits its
+    own rows only (world 1); each rank's result equals the single-process oracle fit of its data."""
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_indep_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for rank in range(2):
+        X, W0, H0, W, H, n_iter = out[rank]
+        Wr, Hr, nr = mu_ref.mu_fit(X, W0, H0, max_iter=50, tol=1e-3)
+        assert n_iter == nr
+        np.testing.assert_allclose(H, Hr, rtol=1e-10, atol=1e-14)
+        np.testing.assert_allclose(W, Wr, rtol=1e-10, atol=1e-14)
 
 
 def test_shard_bounds_cover_rows():
@@ -120,7 +153,7 @@ class _NumpyWeightedPlan(WeightedMUPlan):
         self.k = H.shape[0]
         self.n_out = 2 * self.k * self.F
         self.group = group
-        self.world = dist.get_world_size(group)
+        self.world = plan_world(group)
         self.Wn = np.array(W, dtype=np.float64)
         self.Hn = np.array(H, dtype=np.float64)
         self.AD = torch.zeros(self.n_out, dtype=torch.float64)
@@ -154,7 +187,7 @@ def _wworker(rank, world, port, X, M, W0, H0, max_iter, tol, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         lo, hi = shard_bounds(X.shape[0], world, rank)
-        plan = _NumpyWeightedPlan(X[lo:hi], M[lo:hi], W0[lo:hi], H0)
+        plan = _NumpyWeightedPlan(X[lo:hi], M[lo:hi], W0[lo:hi], H0, group=dist.group.WORLD)
         n_iter = run_mu(plan, max_iter=max_iter, tol=tol)
         out[rank] = (lo, hi, plan.Wn, plan.Hn, n_iter)
     finally:

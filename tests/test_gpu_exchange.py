@@ -73,7 +73,7 @@ def test_self_exchange_is_bit_identical(layout):
     lib.cnmf_set_persist_variant(layout)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
     try:
-        plan = _plan(X, W0, H0)
+        plan = _plan(X, W0, H0, group=dist.group.WORLD)
         plan.enable_exchange()
         assert plan.exchange and plan.persistent
         plan.iterate(10)
@@ -84,7 +84,7 @@ def test_self_exchange_is_bit_identical(layout):
         assert torch.equal(plan.W, ref.W)
         assert torch.equal(plan.H64, ref.H64)
         assert torch.equal(plan.HHt, ref.HHt)
-        assert int(plan.counter.cpu().numpy().astype(np.int64).sum()) == 0
+        assert plan.counters_at_rest()
         plan.release()
     finally:
         dist.destroy_process_group()
@@ -99,7 +99,7 @@ def _rank_main(rank, world, port, N, q):
                                 world_size=world)
         X, W0, H0 = _data(N, 7)
         lo, hi = rank * N // world, (rank + 1) * N // world
-        plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0)
+        plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0, group=dist.group.WORLD)
         plan.enable_exchange()
         plan.iterate(12)
         plan.iterate(18)

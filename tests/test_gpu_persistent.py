@@ -71,7 +71,7 @@ def test_persistent_matches_oracle(n_tiles, layout):
     Ht = plan.Ht.cpu().numpy()
     np.testing.assert_array_equal(Ht[:, :4], H.T)
     np.testing.assert_allclose(plan.HHt.cpu().numpy(), H @ H.T, rtol=1e-12)
-    assert int(plan.counter.cpu().numpy().astype(np.int64).sum()) == 0  # counters back at rest
+    assert plan.counters_at_rest()  # counters back at rest
 
 
 def test_layouts_agree_and_are_deterministic():
@@ -175,7 +175,7 @@ def test_floating_tiles(n_tiles, frac):
             c.iterate(n)
         for p in (a, c):
             p.check_sync_error()
-            assert int(p.counter.cpu().numpy().astype(np.int64).sum()) == 0
+            assert p.counters_at_rest()
     finally:
         lib.cnmf_set_persist_dyn_frac(0.8)
         lib.cnmf_set_persist_variant(old)
@@ -186,3 +186,4 @@ def test_floating_tiles(n_tiles, frac):
         assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
         assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6 and rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
     assert lib.cnmf_set_persist_dyn_frac(0.0) != 0 and lib.cnmf_set_persist_dyn_frac(1.5) != 0
+

@@ -53,7 +53,7 @@ def _worker(rank, world, port, X, W0, H0, n_iter, q):
         from cnmf_amd.distributed import shard_bounds
         from cnmf_amd.solver import MUPlan, run_mu
         lo, hi = shard_bounds(X.shape[0], world, rank)
-        plan = MUPlan(torch.from_numpy(X[lo:hi]).cuda(), 4)
+        plan = MUPlan(torch.from_numpy(X[lo:hi]).cuda(), 4, group=dist.group.WORLD)
         assert plan.world == world
         plan.set_W(torch.from_numpy(W0[lo:hi]))
         plan.set_H(torch.from_numpy(H0))

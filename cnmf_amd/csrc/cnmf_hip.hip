@@ -2070,6 +2070,105 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
 #define TL_START do {} while (0)
 #endif
 
+// The cross-rank all-reduce of AB (k(F+k) fp64) inside a persistent launch, run by the top
+// combiner's NT threads after the rank's own AB is in sAB (LDS) and a.AB.  Each fp64 value travels
+// as two 64-bit words {generation tag : 32-bit half}, written with system-scope atomic stores into
+// slot `rank` of every rank's exchange buffer (remote stores over xGMI); a reader polls its own
+// buffer until every word of every slot carries this generation's tag, so no separate flag, fence or
+// store acknowledgement sits on the critical path.  Slots are summed in rank order: the same AB, bit
+// for bit, on every rank.  Slots alternate by generation parity: rank p writes generation g+2 only
+// after it has read every rank's g+1 words, which each rank writes only after it has read its
+// generation-g slots.  A rank whose launch has failed tags its words XPOISON, which makes every peer
+// fail too (no rank waits out its timeout per iteration).  The thread <-> element mapping is
+// sum_rows_sc1's (o = t, t + NT).  Leaves the summed AB in sAB and a.AB.
+__device__ __forceinline__ void xchg_allreduce_ab(uint64_t* xctl, double* AB, double* sAB, uint32_t* err, int it, int t) {
+  using namespace sl;
+  constexpr int n_out = K * V;
+  static_assert(n_out <= 2 * NT && n_out > NT, "two elements per thread");
+  // atomics: loaded here, not hoisted to the kernel entry
+  const int xrank = (int)__hip_atomic_load(xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int xworld = (int)__hip_atomic_load(xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t gen =
+      (uint32_t)__hip_atomic_load(xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint32_t)it + 1u;
+  auto peer = [&](int r) {
+    return reinterpret_cast<uint64_t*>(
+        __hip_atomic_load(xctl + XC_PEERS + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  TL_X(it, 0);
+  const bool has1 = t + NT < n_out;
+  const size_t slot = 2 * (size_t)n_out;  // words per rank slot
+  const size_t par = (size_t)(gen & 1u) * xworld * slot;
+  {
+    const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    const uint64_t tag = (uint64_t)(bad ? XPOISON : gen) << 32;
+    const uint64_t b0 = (uint64_t)__double_as_longlong(sAB[t]);
+    const uint64_t b1 = has1 ? (uint64_t)__double_as_longlong(sAB[t + NT]) : 0ull;
+    for (int pr = 0; pr < xworld; ++pr) {
+      uint64_t* dst = peer(pr) + par + (size_t)xrank * slot;
+      __hip_atomic_store(dst + 2 * t, tag | (b0 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(dst + 2 * t + 1, tag | (b0 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (has1) {
+        __hip_atomic_store(dst + 2 * (t + NT), tag | (b1 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dst + 2 * (t + NT) + 1, tag | (b1 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  TL_X(it, 1);
+  const uint64_t* mine = peer(xrank) + par;
+  double v0 = 0.0, v1 = 0.0;
+  constexpr int QB = 4;  // ranks polled per round (their loads in flight together)
+  for (int q0 = 0; q0 < xworld; q0 += QB) {
+    uint64_t w[QB][4];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+  #pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
+        w[j][0] = __hip_atomic_load(src + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w[j][1] = __hip_atomic_load(src + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const int o1 = has1 ? t + NT : t;
+        w[j][2] = __hip_atomic_load(src + 2 * o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w[j][3] = __hip_atomic_load(src + 2 * o1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      bool ok = true, poison = false;
+  #pragma unroll
+      for (int j = 0; j < QB; ++j)
+  #pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t tg = (uint32_t)(w[j][m] >> 32);
+          ok = ok && tg == gen;
+          poison = poison || tg == XPOISON;
+        }
+      if (ok) break;
+      if (poison) {
+        __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
+        __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  #pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      if (q0 + j < xworld) {  // rank order
+        v0 += __longlong_as_double((long long)((w[j][1] << 32) | (w[j][0] & 0xFFFFFFFFull)));
+        v1 += __longlong_as_double((long long)((w[j][3] << 32) | (w[j][2] & 0xFFFFFFFFull)));
+      }
+    }
+  }
+  TL_X(it, 2);
+  sAB[t] = v0;
+  st_sc1(AB + t, v0);
+  if (has1) {
+    sAB[t + NT] = v1;
+    st_sc1(AB + t + NT, v1);
+  }
+  TL_X(it, 3);
+}
+
 // WRES: W stays resident in LDS for the whole launch (this workgroup's tiles, loaded once at the
 // start and written back once at the end): the passes stream only X, 324 instead of 356 bytes per
 // sample ("keep tensors resident instead of re-reading them").  Needs nbt·1 KB of extra LDS.
@@ -2333,103 +2432,7 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
       __syncthreads();
       if (sFlag[1] && team == 0) {  // top combiner: AB (team 0; team 1 copies it below)
         sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
-        if (MULTI) {
-          // ---- the cross-rank all-reduce of AB (k(F+k) fp64), inside the launch.  Each fp64
-          // value travels as two 64-bit words {generation tag : 32-bit half} (the LL protocol),
-          // written with system-scope atomic stores into slot `rank` of every rank's exchange
-          // buffer (remote stores over xGMI); a reader polls its own buffer until every word of
-          // every slot carries this generation's tag, so no separate flag, fence or store
-          // acknowledgement sits on the critical path.  Slots are summed in rank order: the same
-          // AB, bit for bit, on every rank.  Slots alternate by generation parity: rank p writes
-          // generation g+2 only after it has read every rank's g+1 words, which each rank writes
-          // only after it has read its generation-g slots.  A rank whose launch has failed tags
-          // its words XPOISON, which makes every peer fail too (no rank waits out its timeout per
-          // iteration).  The thread <-> element mapping is sum_rows_sc1's (o = t, t + NT).
-          constexpr int n_out = K * V;
-          static_assert(n_out <= 2 * NT && n_out > NT, "two elements per thread");
-          // atomics: loaded here, not hoisted to the kernel entry
-          const int xrank = (int)__hip_atomic_load(a.xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int xworld = (int)__hip_atomic_load(a.xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t gen =
-              (uint32_t)__hip_atomic_load(a.xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint32_t)it + 1u;
-          auto peer = [&](int r) {
-            return reinterpret_cast<uint64_t*>(
-                __hip_atomic_load(a.xctl + XC_PEERS + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          };
-          TL_X(it, 0);
-          const bool has1 = t + NT < n_out;
-          const size_t slot = 2 * (size_t)n_out;  // words per rank slot
-          const size_t par = (size_t)(gen & 1u) * xworld * slot;
-          {
-            const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-            const uint64_t tag = (uint64_t)(bad ? XPOISON : gen) << 32;
-            const uint64_t b0 = (uint64_t)__double_as_longlong(sAB[t]);
-            const uint64_t b1 = has1 ? (uint64_t)__double_as_longlong(sAB[t + NT]) : 0ull;
-            for (int pr = 0; pr < xworld; ++pr) {
-              uint64_t* dst = peer(pr) + par + (size_t)xrank * slot;
-              __hip_atomic_store(dst + 2 * t, tag | (b0 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_store(dst + 2 * t + 1, tag | (b0 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              if (has1) {
-                __hip_atomic_store(dst + 2 * (t + NT), tag | (b1 & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                __hip_atomic_store(dst + 2 * (t + NT) + 1, tag | (b1 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              }
-            }
-          }
-          TL_X(it, 1);
-          const uint64_t* mine = peer(xrank) + par;
-          double v0 = 0.0, v1 = 0.0;
-          constexpr int QB = 4;  // ranks polled per round (their loads in flight together)
-          for (int q0 = 0; q0 < xworld; q0 += QB) {
-            uint64_t w[QB][4];
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (true) {
-#pragma unroll
-              for (int j = 0; j < QB; ++j) {
-                const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
-                w[j][0] = __hip_atomic_load(src + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                w[j][1] = __hip_atomic_load(src + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const int o1 = has1 ? t + NT : t;
-                w[j][2] = __hip_atomic_load(src + 2 * o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                w[j][3] = __hip_atomic_load(src + 2 * o1 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              }
-              bool ok = true, poison = false;
-#pragma unroll
-              for (int j = 0; j < QB; ++j)
-#pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                  const uint32_t tg = (uint32_t)(w[j][m] >> 32);
-                  ok = ok && tg == gen;
-                  poison = poison || tg == XPOISON;
-                }
-              if (ok) break;
-              if (poison) {
-                __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-              if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
-              if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
-                __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(1);
-            }
-#pragma unroll
-            for (int j = 0; j < QB; ++j) {
-              if (q0 + j < xworld) {  // rank order
-                v0 += __longlong_as_double((long long)((w[j][1] << 32) | (w[j][0] & 0xFFFFFFFFull)));
-                v1 += __longlong_as_double((long long)((w[j][3] << 32) | (w[j][2] & 0xFFFFFFFFull)));
-              }
-            }
-          }
-          TL_X(it, 2);
-          sAB[t] = v0;
-          st_sc1(a.AB + t, v0);
-          if (has1) {
-            sAB[t + NT] = v1;
-            st_sc1(a.AB + t + NT, v1);
-          }
-          TL_X(it, 3);
-        }
+        if (MULTI) xchg_allreduce_ab(a.xctl, a.AB, sAB, err, it, t);
       }
       if (sFlag[1]) {
         // this iteration's pool is drained (every workgroup's failed draw precedes its ticket):
@@ -2518,6 +2521,405 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
       if (PD == 1) body(q, pfA, pwA);
       else body(q, pfB, pwB);
       if (q + 1 < total && alive) body(q + 1, pfA, pwA);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+}
+
+// ------------------------------------------------------------------------------------------------
+// mu_iter_wt_kernel<PD, MULTI> — the headline shape (fp32 X, F = 81, k = 4) as ONE persistent launch
+// of barrier-free WAVE tiles.
+//
+// Why: the workgroup-tile kernel above (mu_iter_sl_kernel) is issue/latency-bound, not HBM-bound —
+// with X served from L2 it runs at the same 67 µs per iteration (profiles/r02/probes/l2diag.log),
+// its waves park 46 % of their cycles on two workgroup barriers per tile and on one-deep LDS reads
+// of Hᵀ, while a plain streaming read of the same tile shape reaches 7.2 TB/s
+// (profiles/r02/probes/stream_probe*.log).
+//
+// Layout: one 4-wave workgroup per CU, one wave per SIMD (up to 512 VGPRs); every wave owns its own
+// 16-sample tiles gw + NW·i (gw = 4·blockIdx + wave, NW = 4·gridDim) and never waits for another
+// wave inside an iteration.  Lane l = (sample s = l / 4, quarter q = l % 4); q owns features
+// [21q, 21q + 21) (q = 3: 18 real features + 3 zero-Hᵀ pads).
+//  * X: PD tiles (5184 B each) in flight per wave in registers (6 × 16 B per lane, the 6th for
+//    lanes 0-3 only), staged to the wave's private LDS slot (in-order LDS: no barrier) and read
+//    back per lane along its sample row (x kept in 21 VGPRs from phase 1 to phase 3).
+//  * Hᵀ: the lane's 21 × 4 fp32 values and its HHᵀ row (fp64) live in VGPRs for the whole
+//    iteration (reloaded after each basis update) — no Hᵀ read per tile.
+//  * phase 1 (num = x·Hᵀ, SK:543): packed fp32 chains of 7 features folded into fp64 (the sl
+//    arithmetic), then a DPP reduce-scatter inside the quad: lane q ends with num[s][q].
+//  * phase 2 (SK:553-629): the fp64 update of w[s][q] against the LDS-resident W (each wave's tiles
+//    stay in LDS for the whole launch), w' gathered back to the quad by DPP broadcasts.
+//  * phase 3 (A += w'ᵀx, B += w'ᵀw', SK:639-640): packed fp32 accumulators per lane over the
+//    iteration; at its end a DPP / permlane-swap butterfly over the 16 sample lanes of each q,
+//    then the four waves' sums combined in fp64 in a fixed order -> the workgroup's partial row.
+//  * the in-launch reduction (tickets, group / top combiners, flag), the basis update in every
+//    workgroup and the optional cross-rank exchange are those of mu_iter_sl_kernel.
+// ------------------------------------------------------------------------------------------------
+namespace wt {
+constexpr int F = 81, K = 4, V = F + K;
+constexpr int TSW = 16;                 // samples per wave tile
+constexpr int XBW = TSW * F * 4;        // 5184 B of X per wave tile
+constexpr int NCHW = XBW / 16;          // 324 16-byte chunks
+constexpr int PFW = 6;                  // loads per lane per tile (5 × 64 + 4 chunks)
+constexpr int XSTR = XBW + 16;          // per-wave staging stride (16 zero bytes past each tile)
+constexpr int WBW = TSW * K * 4;        // 256 B of W per wave tile
+constexpr int NQ = 21;                  // features per lane
+constexpr int NACC = NQ * K + K;        // 88 fp32 accumulators per lane (A columns + the B row)
+constexpr int NWV = 4;                  // waves per workgroup
+// LDS carve (bytes): the staging slots and the reduction scratch reuse sl's X / W / P regions; the
+// basis state (L_HT, L_HHT, L_H, L_AB, L_FLAG) sits at sl's offsets so sl_update_basis applies
+constexpr int L_STG = 0;                               // [NWV][XSTR]
+constexpr int L_RED = sl::L_P;                         // [NWV][4 q][NACC] fp32
+constexpr int L_WRES = (sl::L_PTOTAL + 15) / 16 * 16;  // [NWV][nbt_max][16][4] fp32
+static_assert(L_STG + NWV * XSTR <= sl::L_P, "staging slots fit below the scratch");
+static_assert(L_RED + NWV * 4 * NACC * 4 <= sl::L_WN + TS * sl::K * 4, "scratch fits sl's P/WN regions");
+static_assert(NCHW == 5 * 64 + 4, "prefetch layout assumes 324 chunks");
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(u & 0xFFFFFFFFll), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// v summed over the 16 lanes l' ≡ l (mod 4) of the wave (all lanes get the sum)
+__device__ __forceinline__ float sum_over_samples(float v) {
+  v += dppf<0x124>(v);  // row_ror:4
+  v += dppf<0x128>(v);  // row_ror:8   -> the row's 4 lanes of this q
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // + lane ^ 16
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);  // + lane ^ 32
+}
+
+// The X prefetch lives in AGPRs and never touches a VGPR: inline-asm loads into AGPR tuples, an
+// asm wait naming them "+a", and asm ds_write_b128 straight from the AGPRs into the staging slot
+// (cdna_hip_programming.md §5.7 item 1, form ii).  Two reasons: (1) hipcc's own counted waits for
+// compiler-issued loads degrade to vmcnt(0) at this loop's header (one tile in flight instead of
+// PD), and (2) under this kernel's VGPR pressure hipcc parks VGPR-resident prefetch registers in
+// AGPRs, copying them before the data has landed.  VMEM returns retire in issue order, so before
+// staging set k, vmcnt(6·(PD-1)) leaves exactly the PD-1 younger sets in flight (compiler-issued
+// memory operations in between only make that wait stricter).
+#ifdef CNMF_X_PLAIN
+#define WT_LD "global_load_dwordx4 %0, %1, off"
+#else
+#define WT_LD "global_load_dwordx4 %0, %1, off nt"
+#endif
+__device__ __forceinline__ void ld16(u32x4& r, const unsigned char* p) {
+  asm volatile(WT_LD : "=a"(r) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_set(u32x4 (&pf)[PFW]) {
+  asm volatile("s_waitcnt vmcnt(%6)"
+               : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5])
+               : "n"(N)
+               : "memory");
+}
+// the tile's 16-byte chunks of this lane: l + 64u (u < 5), and 320 + l for lanes 0-3 (others re-load
+// chunk l: not staged; every lane issues the same six loads)
+__device__ __forceinline__ void prefetch(u32x4 (&pf)[PFW], const unsigned char* __restrict__ X, int64_t tile, int l) {
+#ifdef CNMF_DIAG_L2
+  const unsigned char* xs = X + (size_t)(tile & 255) * XBW + 16 * l;
+#else
+  const unsigned char* xs = X + (size_t)tile * XBW + 16 * l;
+#endif
+#pragma unroll
+  for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
+  ld16(pf[PFW - 1], l < 4 ? xs + 1024 * (PFW - 1) : xs);
+}
+template <int OFF>
+__device__ __forceinline__ void st16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ void stage(unsigned char* stg, const u32x4 (&pf)[PFW], int l) {
+  const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
+  st16<0>(addr, pf[0]);
+  st16<1024>(addr, pf[1]);
+  st16<2048>(addr, pf[2]);
+  st16<3072>(addr, pf[3]);
+  st16<4096>(addr, pf[4]);
+  if (l < 4) st16<5120>(addr, pf[5]);
+}
+}  // namespace wt
+
+template <int PD, bool MULTI = false>
+__global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
+  using namespace wt;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int s = l >> 2, q = l & 3;
+  const int b = blockIdx.x;
+  const int G = gridDim.x;
+  const int NW = NWV * G;
+  const int gw = NWV * b + w;
+  const int NG = a.n_groups;
+  const int g = b % NG;
+  const int gs = (G - g + NG - 1) / NG;
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
+  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);     // this wave's tiles per iteration
+  const int nbt_max = (int)((a.n_tiles + NW - 1) / NW);
+  unsigned char* stg = smem + L_STG + w * XSTR;
+  float* wres = reinterpret_cast<float*>(smem + L_WRES + (size_t)w * nbt_max * WBW);  // [i][16][4]
+  float* red = reinterpret_cast<float*>(smem + L_RED);
+  double* sH = reinterpret_cast<double*>(smem + sl::L_H);
+  double* sAB = reinterpret_cast<double*>(smem + sl::L_AB);
+  int* sFlag = reinterpret_cast<int*>(smem + sl::L_FLAG);
+  uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
+  uint32_t* cnt_top = a.cnt + CNT_TOP;
+  uint32_t* flag = a.cnt + CNT_FLAG;
+  uint32_t* err = a.cnt + CNT_ERR;
+
+  // ---- the basis for the first iteration, the staging pads, this wave's W tiles
+  for (int e = t; e < K * F; e += NT) sH[e] = a.H64[e];
+  if (a.apply_first)
+    for (int e = t; e < K * V; e += NT) sAB[e] = a.AB[e];
+  if (l < 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
+  for (int c = l; c < nbt * (WBW / 16); c += 64) {
+    const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
+    *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
+        *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(a.W) + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
+  }
+  __syncthreads();
+  if (a.apply_first)
+    sl_update_basis(smem, t, a.l1H, a.l2H);
+  else
+    sl_derive_basis(smem, t);
+
+  // the lane's Hᵀ (fp32 pairs: components 0,1 and 2,3 of each of its features) and HHᵀ row q
+  f2 h01[NQ], h23[NQ];
+  double hh[K];
+  auto load_basis = [&]() {
+    const float* sHt = reinterpret_cast<const float*>(smem + sl::L_HT);
+    const double* sHHt = reinterpret_cast<const double*>(smem + sl::L_HHT);
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const float4 h = *reinterpret_cast<const float4*>(sHt + (NQ * q + c) * K);
+      h01[c] = f2{h.x, h.y};
+      h23[c] = f2{h.z, h.w};
+    }
+#pragma unroll
+    for (int m = 0; m < K; ++m) hh[m] = sHHt[q * K + m];
+  };
+  load_basis();
+
+  f2 acc01[NQ], acc23[NQ], accB01, accB23;
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) acc01[c] = acc23[c] = f2{0.f, 0.f};
+    accB01 = accB23 = f2{0.f, 0.f};
+  };
+  zero_acc();
+
+  const int total = a.n_iter * nbt;
+  u32x4 pf[PD][PFW];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) prefetch(pf[k], Xb, gw + (int64_t)NW * k, l);  // the host keeps nbt > PD
+  TL_START;
+
+  bool alive = true;
+  // position counters (wave-uniform, incremental: no division per tile): the tile being processed
+  // (iteration cur_it, index cur_i) and the next one to prefetch (nx_i)
+  int cur_i = 0, cur_it = 0, nx_i = PD;
+  // Every step stages its register set and re-issues it unconditionally (past the launch's last
+  // position: the wave's first tile again, never used), so that the count of younger loads is the
+  // same on every path: staging set k waits vmcnt(6·(PD-1)), i.e. PD tiles stay in flight.
+  auto step = [&](u32x4 (&pfk)[PFW]) {
+    wait_set<PFW * (PD - 1)>(pfk);
+    stage(stg, pfk, l);
+    prefetch(pfk, Xb, gw + (int64_t)NW * nx_i, l);
+    if (++nx_i == nbt) nx_i = 0;
+  };
+  auto body = [&]() {
+    const int it = cur_it, i = cur_i;
+    if (++cur_i == nbt) {
+      cur_i = 0;
+      ++cur_it;
+    }
+    const bool last_it = it + 1 == a.n_iter;
+    // phase 1: x along the lane's row, packed fp32 chains of 7 folded into fp64
+    const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * q;
+    float xv[NQ];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) xv[c] = xr[c];
+    double p0, p1, p2, p3;
+#pragma unroll
+    for (int c0 = 0; c0 < NQ; c0 += 7) {
+      f2 c01 = f2{0.f, 0.f}, c23 = f2{0.f, 0.f};
+#pragma unroll
+      for (int c = c0; c < c0 + 7; ++c) {
+        const f2 xx = f2{xv[c], xv[c]};
+        c01 = __builtin_elementwise_fma(xx, h01[c], c01);
+        c23 = __builtin_elementwise_fma(xx, h23[c], c23);
+      }
+      if (c0 == 0) {
+        p0 = (double)c01.x; p1 = (double)c01.y; p2 = (double)c23.x; p3 = (double)c23.y;
+      } else {
+        p0 += (double)c01.x; p1 += (double)c01.y; p2 += (double)c23.x; p3 += (double)c23.y;
+      }
+    }
+    // quad reduce-scatter: lane q ends with num[s][q] (fp64)
+    const bool hi2 = (q & 2) != 0, hi1 = (q & 1) != 0;
+    double k0 = hi2 ? p2 : p0, k1 = hi2 ? p3 : p1;
+    const double s0 = hi2 ? p0 : p2, s1 = hi2 ? p1 : p3;
+    k0 += dpp64<0x4E>(s0);  // quad_perm [2,3,0,1]
+    k1 += dpp64<0x4E>(s1);
+    const double kk = hi1 ? k1 : k0, ss = hi1 ? k0 : k1;
+    const double num = kk + dpp64<0xB1>(ss);  // quad_perm [1,0,3,2]
+    // phase 2: w[s][q] <- w·num/den (SK:553-629) against the resident W
+    float* wt_ = wres + i * (TSW * K);
+    const float4 wv = *reinterpret_cast<const float4*>(wt_ + s * K);
+    const float wq = hi2 ? (hi1 ? wv.w : wv.z) : (hi1 ? wv.y : wv.x);
+    const double wold = (double)wq;
+    double den = 0.0;
+    den = fma((double)wv.x, hh[0], den);
+    den = fma((double)wv.y, hh[1], den);
+    den = fma((double)wv.z, hh[2], den);
+    den = fma((double)wv.w, hh[3], den);
+    if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
+    if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
+    if (den == 0.0) den = EPS32;                // SK:620
+    const float wn = (float)(wold * (num / den));  // SK:622-629
+    wt_[s * K + q] = wn;
+    const f2 w01 = f2{dppf<0x00>(wn), dppf<0x55>(wn)};  // quad broadcasts of lanes 0, 1
+    const f2 w23 = f2{dppf<0xAA>(wn), dppf<0xFF>(wn)};  // ... and 2, 3
+    // phase 3: A[·][f] += w'·x[f], B[q][·] += w'_q·w' (fp32 per lane over the iteration)
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const f2 xx = f2{xv[c], xv[c]};
+      acc01[c] = __builtin_elementwise_fma(xx, w01, acc01[c]);
+      acc23[c] = __builtin_elementwise_fma(xx, w23, acc23[c]);
+    }
+    accB01 = __builtin_elementwise_fma(f2{wn, wn}, w01, accB01);
+    accB23 = __builtin_elementwise_fma(f2{wn, wn}, w23, accB23);
+    if (i + 1 != nbt) return;
+
+    // ---- end of this wave's iteration: its sums over the 16 sample lanes of each q -> LDS
+    {
+      float* rw = red + (w * 4 + q) * NACC;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        const float4 v = make_float4(sum_over_samples(acc01[c].x), sum_over_samples(acc01[c].y),
+                                     sum_over_samples(acc23[c].x), sum_over_samples(acc23[c].y));
+        if (l < 4) *reinterpret_cast<float4*>(rw + c * K) = v;
+      }
+      const float4 v = make_float4(sum_over_samples(accB01.x), sum_over_samples(accB01.y),
+                                   sum_over_samples(accB23.x), sum_over_samples(accB23.y));
+      if (l < 4) *reinterpret_cast<float4*>(rw + NQ * K) = v;
+    }
+    zero_acc();
+    __syncthreads();
+    // the workgroup's fp64 row [K][V]: the four waves' sums in wave order (deterministic)
+    {
+      double* prow = a.partials + (size_t)b * (K * V);
+      for (int e = t; e < K * V; e += NT) {
+        const int j = e / V;
+        const int v = e - j * V;
+        const int qq = v < F ? v / NQ : j;
+        const int idx = v < F ? (v - NQ * qq) * K + j : NQ * K + (v - F);
+        const float* rr = red + qq * NACC + idx;
+        const double val = ((double)rr[0] + (double)rr[4 * NACC]) + ((double)rr[8 * NACC] + (double)rr[12 * NACC]);
+        __hip_atomic_store(prow + e, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
+    __syncthreads();
+    TL(it, 0);
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
+      sFlag[1] = 0;
+      sFlag[2] = 1;
+    }
+    __syncthreads();
+    if (sFlag[0]) {  // group combiner
+      sum_rows_sc1(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * (K * V), t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
+      }
+      __syncthreads();
+      if (sFlag[1]) {  // top combiner: AB
+        sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_ab(a.xctl, a.AB, sAB, err, it, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0 && !last_it)
+          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TL_PUB(it);
+      }
+    }
+    const bool top = sFlag[1] != 0;
+    if (last_it) {
+      alive = false;
+      // this wave's W back to HBM, once per launch
+      for (int c = l; c < nbt * (WBW / 16); c += 64) {
+        const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+            *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
+      }
+      if (!top) return;
+      // the last combiner of the launch: every other workgroup has arrived for the last time
+      if (a.apply_last) sl_update_basis(smem, t, a.l1H, a.l2H);
+      for (int e = t; e < K * F; e += NT) a.H64[e] = sH[e];
+      for (int e = t; e < F * K; e += NT) {
+        const int f = e / K;
+        const int j = e - f * K;
+        a.Ht[e] = sH[j * F + f];
+      }
+      if (t < K * K) a.HHt[t] = reinterpret_cast<const double*>(smem + sl::L_HHT)[t];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
+        alive = false;
+        return;
+      }
+      for (int e = t; e < K * V; e += NT) sAB[e] = ld_sc1(a.AB + e);
+      __syncthreads();
+    }
+    sl_update_basis(smem, t, a.l1H, a.l2H);
+    load_basis();
+    TL(it, 1);
+  };
+
+  for (int p = 0; p < total && alive; p += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      step(pf[k]);
+      if (p + k < total && alive) body();
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
@@ -3856,13 +4258,14 @@ static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
 // CNMF_TEAMS=1|2 sets the initial value.
 static int initial_variant() {
   const char* v = getenv("CNMF_PERSIST_VARIANT");
-  if (v && (atoi(v) == 2 || atoi(v) == 3)) return atoi(v);
-  return (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 1;
+  if (v && atoi(v) >= 1 && atoi(v) <= 4) return atoi(v);
+  return (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 4;
 }
 static std::atomic<int> g_persist_variant{initial_variant()};
 
 int cnmf_set_persist_variant(int v) {
-  if (v < 1 || v > 3) return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs), 2 (teams) or 3 (pairs + floating tiles)");
+  if (v < 1 || v > 4)
+    return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs), 2 (teams), 3 (pairs + floating tiles) or 4 (wave tiles)");
   g_persist_variant.store(v);
   return CNMF_OK;
 }
@@ -3991,7 +4394,42 @@ int cnmf_xbuf_free(void* dptr) {
   return CNMF_OK;
 }
 
-// one cooperative launch of mu_iter_sl_kernel
+// ---- variant 4: barrier-free wave tiles (mu_iter_wt_kernel<PD, MULTI>: one 4-wave workgroup per
+// CU, each wave on its own 16-sample tiles, W resident in LDS).  CNMF_WT_PD = prefetch depth (2-4).
+static int wt_pd() {
+  const char* v = getenv("CNMF_WT_PD");
+  const int pd = v ? atoi(v) : 3;
+  return pd >= 2 && pd <= 4 ? pd : 3;
+}
+static PassFn wt_fn(bool multi) {
+  switch (wt_pd()) {
+    case 2: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<2, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<2, false>);
+    case 4: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, false>);
+    default: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<3, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<3, false>);
+  }
+}
+// workgroups (0: not eligible) and LDS bytes of a wave-tile launch over n_rows (a persistent shape)
+static int64_t wt_grid(int64_t n_rows, bool multi, size_t* lds_out) {
+  if (g_persist_variant.load() != 4 || n_rows % wt::TSW != 0) return 0;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  const int64_t n_tiles = n_rows / wt::TSW;
+  const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * (wt_pd() + 1)), (int64_t)sl::GROUP * sl::MAX_GROUPS});
+  if (G < 1) return 0;
+  const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
+  const size_t lds = (size_t)wt::L_WRES + (size_t)wt::NWV * nbt_max * wt::WBW;
+  if (lds > kMaxLds) return 0;
+  const PassFn fn = wt_fn(multi);
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
+  if (per_cu < 1 || G > (int64_t)per_cu * ncu) return 0;  // the whole grid must be co-resident
+  *lds_out = lds;
+  return G;
+}
+
+// one plain launch of mu_iter_sl_kernel
 static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, double* H64, double* Ht,
                              double* HHt, double* partials, int64_t n_parts, double* stage,
                              uint32_t* counter, double* AB, int64_t n_rows, double l1_W, double l2_W,
@@ -4022,6 +4460,16 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.xctl = xctl;
   const bool multi = xctl != nullptr;
   void* args[] = {&pa};
+  {
+    size_t wlds_wt = 0;
+    const int64_t GW = wt_grid(n_rows, multi, &wlds_wt);
+    if (GW > 0 && GW <= n_parts) {
+      pa.n_tiles = n_rows / wt::TSW;
+      pa.n_groups = (int)((GW + sl::GROUP - 1) / sl::GROUP);
+      HIP_CHECK(hipLaunchKernel(wt_fn(multi), dim3((unsigned)GW), dim3(NT), args, wlds_wt, s));
+      return CNMF_OK;
+    }
+  }
   if (n_iter > 1) {
     size_t tlds = 0;
     const int64_t GT = persist_teams_grid(n_rows / TS, multi, &tlds);

@@ -303,17 +303,18 @@ class MUPlan:
             self._allreduce(self.AB)
         self.basis_update()
 
-    def tune(self, n_iter: int = 100, rounds: int = 2) -> dict:
-        """Time the layouts of the persistent launch (cnmf_set_persist_variant: 1 = pairs of
-        4-wave workgroups, 2 = 8-wave two-team workgroups, 3 = pairs with floating tiles) on this
-        plan's shape and keep the fastest for the process.  Runs on copies of W and H: the plan's state is unchanged.  Call after
-        the GPU has been busy for a while (the clock ramps up over the first ~35 ms of work).
-        Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent plans."""
+    def tune(self, n_iter: int = 100, rounds: int = 2, variants=(4, 1, 2)) -> dict:
+        """Time the layouts of the persistent launch (cnmf_set_persist_variant: 4 = wave tiles,
+        1 = pairs of 4-wave workgroups, 2 = 8-wave two-team workgroups; 3 = pairs with floating
+        tiles is not bit-repeatable and only timed when asked for) on this plan's shape and keep
+        the fastest for the process.  Runs on copies of W and H: the plan's state is unchanged.
+        Call after the GPU has been busy for a while (the clock ramps up over the first ~35 ms of
+        work).  Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent
+        plans."""
         if not self.persistent:
             return {}
         W0, H0 = self.W.clone(), self.H64.clone()
         stream = torch.cuda.current_stream(self.device)
-        variants = (1, 2, 3)
         times = {v: [] for v in variants}
         try:
             for _ in range(rounds):

@@ -105,14 +105,17 @@ int cnmf_counter_err_word(void);
  * iteration. */
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
 
-/* Process-wide layout of multi-iteration persistent launches (results agree to fp32 rounding of
- * the per-workgroup partial sums, not bit for bit): 1 = two independent 4-wave workgroups per CU
- * (default), 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart,
+/* Process-wide layout of persistent launches (results agree to fp32 rounding of the partial sums,
+ * not bit for bit): 4 = wave tiles (default): one 4-wave workgroup per CU, each wave streaming its
+ * own 16-sample tiles with no barrier inside an iteration, W resident in LDS (CNMF_WT_PD = 2..4
+ * tiles in flight per wave, default 3); 1 = two independent 4-wave workgroups per CU on 64-sample
+ * tiles, 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart,
  * 3 = layout 1 with floating tiles: a fraction `frac` of the tiles stays with its workgroup (W
  * resident), the rest is drawn from a pool every iteration so that faster CUs take more (not
- * bit-repeatable: the draw decides the summation order).  The fastest differs between boxes;
- * MUPlan.tune() times them and sets it.  cnmf_set_persist_dyn_frac: frac in (0, 1] (default 0.8,
- * env CNMF_DYN_FRAC); a shape with fewer than 4 static tiles per workgroup uses layout 1. */
+ * bit-repeatable: the draw decides the summation order).  MUPlan.tune() times 4, 1 and 2 and keeps
+ * the fastest.  cnmf_set_persist_dyn_frac: frac in (0, 1] (default 0.8, env CNMF_DYN_FRAC); a shape
+ * with fewer than 4 static tiles per workgroup uses layout 1, one whose W does not fit LDS under
+ * layout 4 uses layout 1. */
 int cnmf_set_persist_variant(int variant);
 int cnmf_get_persist_variant(void);
 int cnmf_set_persist_dyn_frac(double frac);

@@ -46,7 +46,7 @@ def _plan(X, W0, H0, group=None):
     return plan
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["pairs", "teams", "floating"])
+@pytest.fixture(params=[4, 1, 2, 3], ids=["wave", "pairs", "teams", "floating"])
 def layout(request):
     """Every persistent layout a rank may pick (MUPlan.tune runs them all at N > 1 too); the
     multi-GPU launch serves layout 3 with layout 1 (floating tiles are single-GPU only)."""

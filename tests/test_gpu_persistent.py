@@ -35,7 +35,7 @@ def _unfused(plan, n):
         plan.basis_update()
 
 
-@pytest.fixture(params=[1, 2, 3], ids=["pairs", "teams", "floating"])
+@pytest.fixture(params=[4, 1, 2, 3], ids=["wave", "pairs", "teams", "floating"])
 def layout(request):
     """The persistent launch's layouts (cnmf_set_persist_variant): pairs of 4-wave workgroups per
     CU, one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart), or pairs with
@@ -86,7 +86,7 @@ def test_layouts_agree_and_are_deterministic():
     W0, H0 = random_init(X, 4, 5)
     out = {}
     try:
-        for v in (1, 2):
+        for v in (4, 1, 2):
             lib.cnmf_set_persist_variant(v)
             a, c = _plan(X, W0, H0), _plan(X, W0, H0)
             a.iterate(60)
@@ -98,7 +98,8 @@ def test_layouts_agree_and_are_deterministic():
             out[v] = (a.W.cpu().numpy(), a.H64.cpu().numpy())
     finally:
         lib.cnmf_set_persist_variant(old)
-    assert rel_fro(out[1][0], out[2][0]) < 1e-6 and rel_fro(out[1][1], out[2][1]) < 1e-6
+    for v in (2, 4):
+        assert rel_fro(out[1][0], out[v][0]) < 1e-6 and rel_fro(out[1][1], out[v][1]) < 1e-6
 
 
 def test_persistent_agrees_with_per_iteration_launches():

@@ -62,6 +62,10 @@ def parse():
                    help="multi-GPU MU: auto = the all-reduce inside the persistent launch (peer "
                         "exchange over xGMI), validated against the RCCL path before timing and "
                         "replaced by it on any failure; off = shard step + RCCL all_reduce")
+    p.add_argument("--ramp-seconds", type=float, default=0.5,
+                   help="untimed clock ramp after the warmup: iterations on copies of W and H until "
+                        "this much GPU time has passed (the chip holds a low clock for its first "
+                        "tens of ms of work; the state is restored, the timed K steps are unchanged)")
     p.add_argument("--no-tune", action="store_true",
                    help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -258,8 +262,28 @@ def main():
             plan.iterate(args.warmup)
             torch.cuda.synchronize()
 
-    # the persistent launch has two layouts whose order differs between boxes: time both on this
-    # box (warm clocks; copies of W / H, so the state is unchanged) and keep the faster
+    # clock ramp: after idle the chip runs its first tens of ms of work at lower clocks (r01/r02:
+    # a 20-step timing after a 5-step warmup read 66 us per iteration against 57-58 us once warm);
+    # run untimed iterations on copies of W / H until ramp_s of GPU time has passed
+    ramp_s = 0.0
+    if args.ramp_seconds > 0:
+        import torch as _t
+        W_keep = plan.W.clone()
+        H_keep = plan.H64.clone()
+        t_r = time.perf_counter()
+        while time.perf_counter() - t_r < args.ramp_seconds:
+            plan.iterate(100)
+            _t.cuda.synchronize()
+        ramp_s = time.perf_counter() - t_r
+        plan.W.copy_(W_keep)
+        plan.H64.copy_(H_keep)
+        if hasattr(plan, "refresh_basis"):
+            plan.refresh_basis()
+        _t.cuda.synchronize()
+        plan.check_sync_error()
+
+    # the persistent launch has several layouts whose order can differ between boxes: time them on
+    # this box (warm clocks; copies of W / H, so the state is unchanged) and keep the fastest
     tuned = {}
     if args.solver == "mu" and plan.persistent and not args.no_tune:
         tuned = plan.tune(n_iter=100, rounds=2)
@@ -347,12 +371,15 @@ def main():
         kname = "weighted MU pass (wmu_pass_kernel: W-step + [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))])"
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
-    elif persistent and world == 1:
-        kname = ("mu_iter_sl_kernel (persistent: K iterations of pass + in-launch reduction + basis "
-                 "update per launch)")
     elif persistent:
-        kname = ("mu_iter_sl_kernel<..., MULTI> (persistent, one launch per rank: K iterations of "
-                 "pass + in-launch reduction + peer all-reduce over xGMI + basis update)")
+        variant = int(plan.lib.cnmf_get_persist_variant())
+        kbase = "mu_iter_wt_kernel" if variant == 4 else "mu_iter_sl_kernel"
+        if world == 1:
+            kname = (f"{kbase} (persistent: K iterations of pass + in-launch reduction + basis "
+                     "update per launch)")
+        else:
+            kname = (f"{kbase}<..., MULTI> (persistent, one launch per rank: K iterations of "
+                     "pass + in-launch reduction + peer all-reduce over xGMI + basis update)")
     elif plan.persistent_shape:
         kname = ("mu_iter_sl_kernel shard step (one iteration per launch: pending basis update, "
                  "pass, in-launch reduction; all_reduce between launches)")
@@ -414,7 +441,8 @@ def main():
                                   + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
                    "exchange": exchange,
                    "persistent_layout": layout if plan.persistent else None,
-                   "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None},
+                   "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None,
+                   "clock_ramp_s": round(ramp_s, 3)},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

@@ -3524,7 +3524,11 @@ static int64_t max_resident(PassFn fn, size_t lds) {
   int per_cu = 0, ncu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return -1;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-  per_cu = std::max(1, std::min(per_cu, 8));
+  // MI355X_MICROARCH.md "Correctness boundaries": the occupancy API reports one block per CU too
+  // many for kernels of 81-112 SGPRs; every kernel here stays <= 112, whose residency is
+  // min(API, 8, floor(800 / (112 + 16))) = at most 6 256-thread blocks per CU
+  per_cu = std::min(per_cu, std::min(8, 800 / (112 + 16)));
+  if (per_cu < 1) return 0;
   int64_t v = (int64_t)per_cu * ncu;
   std::lock_guard<std::mutex> lk(g_occ_mu);
   g_occ[key] = v;
@@ -4409,22 +4413,24 @@ static PassFn wt_fn(bool multi) {
   }
 }
 // workgroups (0: not eligible) and LDS bytes of a wave-tile launch over n_rows (a persistent shape)
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus[dev] = 0;
+  return cus[dev];
+}
 static int64_t wt_grid(int64_t n_rows, bool multi, size_t* lds_out) {
   if (g_persist_variant.load() != 4 || n_rows % wt::TSW != 0) return 0;
-  int dev = 0, ncu = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  const int ncu = device_cus();
   const int64_t n_tiles = n_rows / wt::TSW;
   const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * (wt_pd() + 1)), (int64_t)sl::GROUP * sl::MAX_GROUPS});
   if (G < 1) return 0;
   const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
   const size_t lds = (size_t)wt::L_WRES + (size_t)wt::NWV * nbt_max * wt::WBW;
   if (lds > kMaxLds) return 0;
-  const PassFn fn = wt_fn(multi);
-  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return 0;
-  if (per_cu < 1 || G > (int64_t)per_cu * ncu) return 0;  // the whole grid must be co-resident
+  // co-residency of the whole grid (cached per kernel and LDS size; sets the LDS attribute once)
+  if (max_resident(wt_fn(multi), lds) < G) return 0;
   *lds_out = lds;
   return G;
 }

@@ -37,10 +37,7 @@ def main():
     fn = lib.cnmf_debug_timeline
     fn.argtypes = [ctypes.c_void_p]
     fn.restype = ctypes.c_int
-    plan = MUPlan(torch.from_numpy(X).cuda(), 4)
-    plan.set_W(torch.from_numpy(W0))
-    plan.set_H(torch.from_numpy(H0))
-    assert plan.persistent
+    group = None
     if a.exchange:
         import socket
         import torch.distributed as dist
@@ -48,7 +45,13 @@ def main():
             so.bind(("127.0.0.1", 0))
             port = so.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        group = dist.group.WORLD
+    plan = MUPlan(torch.from_numpy(X).cuda(), 4, group=group)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    if a.exchange:
         plan.enable_exchange()
+    assert plan.persistent
     plan.iterate(a.warmup)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

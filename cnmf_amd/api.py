@@ -28,11 +28,9 @@ from .synthetic import random_init
 
 __all__ = ["factorise", "fit", "non_negative_factorization", "NMF", "ConvergenceWarning"]
 
-try:  # keep sklearn's warning class when it is importable (drop-in); never required
-    from sklearn.exceptions import ConvergenceWarning  # type: ignore
-except Exception:  # pragma: no cover
-    class ConvergenceWarning(UserWarning):
-        """Custom warning to capture convergence problems (sklearn.exceptions.ConvergenceWarning)."""
+class ConvergenceWarning(UserWarning):
+    """Custom warning to capture convergence problems (the role of
+    sklearn.exceptions.ConvergenceWarning; the product path imports nothing from sklearn)."""
 
 _INITS = {"random", "nndsvd", "nndsvda", "nndsvdar", "custom", None}
 

@@ -4509,8 +4509,16 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
                        int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
                        double l2_H, int apply_first, void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-  if (!X || !W || !H64 || !Ht || !HHt || !stage || !counter || !AB)
+  if ((n_rows > 0 && (!X || !W)) || !H64 || !Ht || !HHt || !stage || !counter || !AB)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_rows == 0) {  // an empty shard (world > rows): the pending update, then zeros for the all-reduce
+    if (apply_first) {
+      const int st = cnmf_basis_update(AB, H64, Ht, HHt, n_features, k, l1_H, l2_H, 1, nullptr, stream);
+      if (st) return st;
+    }
+    HIP_CHECK(hipMemsetAsync(AB, 0, sizeof(double) * k * (n_features + k), hs));
+    return CNMF_OK;
+  }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G > 0) {
@@ -4555,7 +4563,10 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
   if (st) return st;
   const int64_t nb = cnmf_pass_blocks(n_rows, n_features, k, x_dtype);
   if (nb < 0) return (int)nb;
-  if (nb == 0) return CNMF_OK;
+  if (nb == 0) {  // no rows: this shard contributes zeros to the all-reduce
+    HIP_CHECK(hipMemsetAsync(AB, 0, sizeof(double) * k * (n_features + k), hs));
+    return CNMF_OK;
+  }
   return cnmf_reduce_partials(partials, nb, k * (n_features + k), stage, counter, AB, stream);
 }
 
@@ -4657,7 +4668,8 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
                          int64_t n_parts, int64_t n_rows, int n_features, int k, int flags, void* stream) {
   const int64_t G = cnmf_wmu_pass_blocks(n_rows, n_features, k);
   if (G < 0) return (int)G;
-  if (!X || !M || !W || !H64 || (G > 0 && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (G == 0) return CNMF_OK;  // no rows (an empty shard): nothing to read or write
+  if (!X || !M || !W || !H64 || !partials) return set_err(CNMF_ERR_ARG, "null pointer argument");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(M) & 15) ||
       (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X, the weights and W must be 16-byte aligned");

@@ -88,6 +88,9 @@ def load_spectra(path, *, columns=None, dtype=np.float32, device=None, chunk_row
     done = [None, None]
     lo = 0
     with torch.cuda.device(device):
+        # `out` was allocated on the current stream: the side stream's copies into it must follow
+        # whatever work the caching allocator's recycled block may still have queued there
+        side.wait_stream(torch.cuda.current_stream(device))
         for i, part in enumerate(gen(chunk_rows)):
             m = part.shape[0]
             b = i & 1

@@ -4,7 +4,13 @@ Restates sklearn 1.7.2's `_initialize_nmf` (SK:221-373) — 'random' (SK:303-314
 NNDSVD family (SK:317-373) — together with the randomized SVD it calls
 (`sklearn/utils/extmath.py`: `_randomized_range_finder` :287-357, `_randomized_svd` :530-604,
 `svd_flip` :900-953) op for op in NumPy/SciPy, so a NumPy X gives the same (W0, H0) as sklearn
-for the same random_state.  The hot loop never runs here; a GPU NNDSVD is SURVEY.md §8(f4).
+for the same random_state.  The hot loop never runs here; the GPU NNDSVD is
+`cnmf_amd.gpu_init`.
+
+Attribution: the NNDSVD and randomized-SVD code below is a transcription of scikit-learn's
+(BSD 3-Clause License, Copyright (c) 2007-2024 The scikit-learn developers; the license text ships
+with scikit-learn as sklearn/COPYING): keeping its arithmetic op for op is what makes the host init
+bit-identical to the reference's declared solver library.
 """
 from __future__ import annotations
 

@@ -232,6 +232,11 @@ class MUPlan:
                                              None, self._stream()), "cnmf_basis_update")
 
     def shard_step(self, apply_first: bool):
+        if self.n_rows == 0:  # an empty shard (world > rows): the pending update, then zeros
+            if apply_first:
+                self.basis_update()
+            self.AB.zero_()
+            return
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_mu_shard_step(
                 _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
@@ -280,6 +285,13 @@ class MUPlan:
                     _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
                     self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl),
                     *_event_array(pass_events), self._stream()), "cnmf_mu_iterations_multi")
+            return
+        if self.world == 1 and not self.shard_steps and self.persistent_shape and not self.persistent:
+            # kept off the persistent kernel (a launch of it failed): pass + reduce + update launches
+            for _ in range(n_iter):
+                self.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
+                self.reduce(self.n_out, self.AB)
+                self.basis_update()
             return
         if self.world == 1 and not self.shard_steps:
             with torch.cuda.device(self.device):
@@ -352,13 +364,38 @@ class MUPlan:
 
     def frobenius_error(self) -> float:
         """sqrt(‖X − W·H‖²) over all ranks (SK:85-129 with square_root=True); synchronises."""
-        self.sample_pass(_lib.PASS_LOSS)
-        self.reduce(1, self.loss_buf)
+        if self.n_rows == 0:
+            self.loss_buf.zero_()
+        else:
+            self.sample_pass(_lib.PASS_LOSS)
+            self.reduce(1, self.loss_buf)
         self._allreduce(self.loss_buf)
         return math.sqrt(max(float(self.loss_buf.item()), 0.0))
 
     def H(self, dtype=None) -> torch.Tensor:
         return self.H64.to(dtype or self.tc)
+
+
+def _iterate_guarded(plan, n_iter: int, update_H: bool):
+    """plan.iterate(n_iter) for a persistent plan, with a way back: W and H are snapshotted before
+    the launch; if it reports a synchronisation failure (a workgroup never co-resident, a peer rank
+    timed out: HipLibraryError from check_sync_error, results invalid), the snapshot is restored and
+    the stretch re-run on the per-iteration path (single GPU) or the RCCL path (multi-GPU; every
+    rank fails the same launch, the exchange poisons its peers).  Synchronises."""
+    import warnings
+    W0, H0 = plan.W.clone(), plan.H64.clone()
+    plan.iterate(n_iter, update_H)
+    try:
+        plan.check_sync_error()
+    except _lib.HipLibraryError as e:
+        warnings.warn(f"{e}; the stretch is re-run on the per-iteration path", RuntimeWarning)
+        plan.W.copy_(W0)
+        plan.H64.copy_(H0)
+        plan.refresh_basis()
+        plan.exchange = False
+        plan.persistent = False
+        plan.iterate(n_iter, update_H)
+        plan.check_sync_error()
 
 
 def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool = True,
@@ -373,10 +410,13 @@ def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool 
     it = 0
     while it < max_iter:
         stop = min(max_iter, (it // 10 + 1) * 10) if tol > 0 else max_iter
-        plan.iterate(stop - it, update_H)
+        if getattr(plan, "persistent", False) and update_H:
+            _iterate_guarded(plan, stop - it, update_H)
+        else:
+            plan.iterate(stop - it, update_H)
+            if tol > 0 or stop >= max_iter:
+                plan.check_sync_error()
         it = stop
-        if tol > 0 or it >= max_iter:
-            plan.check_sync_error()
         if tol > 0 and it % 10 == 0:  # SK:872-884
             error = plan.frobenius_error()
             errors.append((it, error))
@@ -499,6 +539,8 @@ class WeightedMUPlan:
         return self.H64.to(dtype or self.tc)
 
     def sample_pass(self, flags: int):
+        if self.n_rows == 0:  # an empty shard: reduce() contributes zeros
+            return
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_wmu_sample_pass(
                 _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64), _ptr(self.partials),

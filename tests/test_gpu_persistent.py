@@ -188,3 +188,26 @@ def test_floating_tiles(n_tiles, frac):
         assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6 and rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
     assert lib.cnmf_set_persist_dyn_frac(0.0) != 0 and lib.cnmf_set_persist_dyn_frac(1.5) != 0
 
+
+
+def test_failed_persistent_launch_falls_back():
+    """a persistent launch that reports a synchronisation failure (forced here
+    by a set error word: every waiting workgroup gives up) leaves invalid results; run_mu restores
+    the W / H snapshot, re-runs the stretch on the per-iteration path and still matches the oracle."""
+    import warnings
+    from cnmf_amd.solver import run_mu
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(64 * 1000, 81, seed=31, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 8)
+    plan = _plan(X, W0, H0)
+    assert plan.persistent
+    plan.counter[plan.err_word] = 1
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        n = run_mu(plan, max_iter=40, tol=0.0)
+    assert n == 40 and any("re-run" in str(r.message) for r in rec)
+    assert not plan.persistent and plan.counters_at_rest()
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=40, tol=0.0)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))

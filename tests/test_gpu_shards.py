@@ -44,7 +44,7 @@ def test_shard_steps_match_single_gpu(N):
     assert rel_fro(a.H64.cpu().numpy(), b.H64.cpu().numpy()) < 1e-6
 
 
-def _worker(rank, world, port, X, W0, H0, n_iter, q):
+def _worker(rank, world, port, X, W0, H0, n_iter, q, tol=1e-4):
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -57,7 +57,7 @@ def _worker(rank, world, port, X, W0, H0, n_iter, q):
         assert plan.world == world
         plan.set_W(torch.from_numpy(W0[lo:hi]))
         plan.set_H(torch.from_numpy(H0))
-        n = run_mu(plan, max_iter=n_iter, tol=1e-4)
+        n = run_mu(plan, max_iter=n_iter, tol=tol)
         q.put((rank, lo, hi, plan.W.cpu().numpy(), plan.H64.cpu().numpy(), n))
     finally:
         dist.destroy_process_group()
@@ -87,6 +87,31 @@ def test_two_process_shards_match_oracle():
                                max_iter=200, tol=1e-4)
     assert res[0][5] == nr
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_two_process_with_an_empty_shard():
+    """world > rows: rank 1 owns no row; its shard contributes zeros to every all_reduce
+    and still applies the identical basis update."""
+    import torch.multiprocessing as mp
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1, 81, seed=6, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, X, W0, H0, 60, q, 1e-3)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in procs)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[1][1] == res[1][2]  # rank 1's shard is empty
+    assert np.array_equal(res[0][4], res[1][4]) and res[0][5] == res[1][5]
+    Wr, Hr, nr = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                               max_iter=60, tol=1e-3)
+    assert res[0][5] == nr
+    assert rel_fro(res[0][3], Wr) <= 1e-5 and rel_fro(res[0][4], Hr) <= 1e-5
 
 
 def _wworker(rank, world, port, X, M, W0, H0, n_iter, q):

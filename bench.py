@@ -1,22 +1,26 @@
-"""Benchmark of the MI355X MU hot path (BASELINE.json metric, configs[1] = cfg2 per GPU).
+"""Benchmark of the MI355X MU hot path (BASELINE.json metric: MU iterations/sec & achieved HBM
+GB/s vs peak, V = 1e6 x 81, k = 4, at 1/2/4/8 GPUs; configs[1] = cfg2 at one GPU).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
-    python bench.py --solver als            # cfg5, the constrained ALS
+    python bench.py --rows 10000000 --k 8             # cfg3 (its 8-GPU run: --gpus 8 via torchrun)
+    python bench.py --scaling weak                    # every GPU owns 1e6 rows (aggregate line)
+    python bench.py --solver als                      # cfg5, the constrained ALS
     python bench.py --features 300 --k 16 --dtype bf16   # cfg4, the bf16 matrix-core pass
 
 One "step" = one MU iteration (sample pass over X + cross-workgroup reduction + basis update) on
-synthetic IOP spectra (cnmf_amd.synthetic), V = 1e6 x 81 per GPU, k = 4, fp32, tol = 0, inputs
-resident in HBM before the timed region.  Multi-GPU is weak scaling: each rank owns a 1e6-row shard
-and the k·(F+k) fp64 accumulators are all-reduced once per iteration (RCCL, backend "nccl").
-
-value = sum over ranks of (shard rows / 1e6) × iterations / wall seconds, i.e. MU iterations per
-second on a 1e6 x 81 problem (exactly it/s at N = 1; the whole-job aggregate at N > 1).
+synthetic IOP spectra (cnmf_amd.synthetic), fp32, tol = 0, inputs resident in HBM before the timed
+region.  Default --scaling strong: V = --rows x 81 (1e6 x 81) is ONE problem whose rows are split
+over the N ranks in 64-row-aligned shards; the k(F+k) fp64 accumulators are all-reduced once per
+iteration (inside the persistent launch over xGMI when validated, else RCCL); value = iterations
+per second of that problem (exactly cfg2's it/s at N = 1).  --scaling weak: every rank owns --rows
+rows, value = sum over ranks of (rows / 1e6) x iterations / s.
 
 Extra keys: roofline (the dominant kernel timed with HIP events on its launch stream inside the
 timed region: at N = 1 the ONE persistent launch that runs all K iterations, else each per-iteration
-launch; achieved = algorithmic bytes N·(F·4 + 2·k·4) per iteration × iterations per launch ÷ launch
-time), cpu_baseline (the NumPy / scipy oracle, rank 0 at N = 1 only, bounded sample).
+launch; achieved = algorithmic bytes of this GPU's shard n·(F·4 + 2·k·4) per iteration × iterations
+per launch ÷ the slowest rank's launch time, peak = one MI355X's 8 TB/s), cpu_baseline (the NumPy /
+scipy oracle, rank 0 at N = 1 only, bounded sample).
 """
 from __future__ import annotations
 
@@ -42,7 +46,12 @@ def parse():
     # lower clocks (tools/bench_trend.py: 73.7 us/iteration on the first 500-iteration launch,
     # 66 us on the following ones), so a short warmup would time the clock ramp, not the solver
     p.add_argument("--warmup", type=int, default=1000)
-    p.add_argument("--rows", type=int, default=1_000_000, help="rows per GPU")
+    p.add_argument("--rows", type=int, default=1_000_000,
+                   help="rows of V: the whole problem (--scaling strong) or per GPU (--scaling weak)")
+    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                   help="strong (default): the BASELINE metric's fixed V (1e6 x 81) split over the "
+                        "GPUs, value = iterations/s of that problem; weak: every GPU owns --rows "
+                        "rows, value = iterations/s of a 1e6-row problem summed over GPUs")
     p.add_argument("--features", type=int, default=81)
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
@@ -161,7 +170,10 @@ def validate_exchange(plan, W0, H0d, n=20):
     dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
     dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
     same = bool(torch.equal(hmax, hmin))
-    bad = fail or (not same) or not (dH < 1e-9 and dW < 1e-5)
+    # the two paths may run different kernels (the exchange: the persistent launch; RCCL: one
+    # shard-step launch per iteration), whose fp32 partial sums are grouped differently: agreement
+    # to that noise, the parity bar's hundredth
+    bad = fail or (not same) or not (dH < 1e-6 and dW < 1e-6)
     st = torch.tensor([1.0 if bad else 0.0, dH, dW], dtype=torch.float64, device=dev)
     dist.all_reduce(st, op=dist.ReduceOp.MAX)
     plan.set_W(torch.from_numpy(W0))
@@ -215,8 +227,15 @@ def main():
     from cnmf_amd.solver import ALSPlan, MUPlan, WeightedMUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
 
-    n_rows, F, k = args.rows, args.features, args.k
+    F, k = args.features, args.k
+    if args.scaling == "strong":  # the fixed problem, 64-row-aligned shards (persistent tiles)
+        from cnmf_amd.distributed import shard_bounds
+        lo, hi = shard_bounds(args.rows, world, rank, align=64)
+        n_rows = hi - lo
+    else:
+        n_rows = args.rows
     np_dt = np.float64 if args.dtype == "f64" else np.float32
+    # synthetic spectra per shard (seed = rank: at N = 1 exactly cfg2's X); H0 is rank 0's
     X = iop_spectra(n_rows, F, seed=rank, dtype=np_dt)
     W0, H0 = random_init(X, k, 42 + rank)
     Xt = torch.from_numpy(X)
@@ -353,7 +372,7 @@ def main():
     bytes_per_pass = n_rows * (F * sx + 2 * k * sw) + (n_rows * F * 4 if args.weighted else 0)  # + M
     iters_per_launch = K if persistent else 1
     bytes_per_launch = bytes_per_pass * iters_per_launch
-    achieved = bytes_per_launch / avg_pass_s / 1e9
+    achieved = bytes_per_launch / avg_pass_s_max / 1e9
 
     # sanity of the measured state (cheap): the objective is finite, W/H non-negative
     err = plan.frobenius_error()
@@ -403,8 +422,10 @@ def main():
         else:
             cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
 
-    total_units = world * n_rows / 1e6
-    value = total_units * K / elapsed
+    if args.scaling == "strong":
+        value = K / elapsed  # iterations per second of the whole (fixed) problem
+    else:
+        value = world * n_rows / 1e6 * K / elapsed
     if args.weighted:
         metric = "weighted MU iterations/sec (V=1e6x81 k=4 with per-element weights, 30 % zero)"
         workload = (f"weighted / masked MU (SURVEY 8f row 2, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
@@ -416,11 +437,20 @@ def main():
                     f"lambda={args.smoothness} NNLS basis sweep, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
                     f"{args.dtype} synthetic IOP spectra")
     else:
-        metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
-        cfg = {(1_000_000, 81, 4, "f32"): "cfg2", (1_250_000, 81, 8, "f32"): "cfg3 (one GPU's shard)",
-               (1_000_000, 300, 16, "bf16"): "cfg4"}.get((n_rows, F, k, args.dtype), "custom")
-        workload = (f"{cfg}: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
-                    f"{args.dtype} synthetic IOP spectra; rows sharded across GPUs")
+        cfg = {(1_000_000, 81, 4, "f32"): "cfg2", (10_000_000, 81, 8, "f32"): "cfg3",
+               (1_250_000, 81, 8, "f32"): "cfg3 (one GPU's shard)",
+               (1_000_000, 300, 16, "bf16"): "cfg4"}.get((args.rows, F, k, args.dtype), "custom")
+        if args.scaling == "strong":
+            metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6\u00d781 k=4, 1/2/4/8 GPU"
+                      if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
+            workload = (f"{cfg}: MU (Frobenius, tol=0) on V={args.rows}x{F} in total, k={k}, "
+                        f"{args.dtype} synthetic IOP spectra, rows split over {world} GPU(s) in "
+                        f"64-row-aligned shards (strong scaling: the problem is fixed)")
+        else:
+            metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
+            workload = (f"{cfg}: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+                        f"{args.dtype} synthetic IOP spectra (weak scaling: every GPU owns this "
+                        f"many rows)")
     out = {
         "metric": metric,
         "value": round(value, 2),
@@ -430,11 +460,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / K * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f64": "f64", "bf16": "bf16 X / f32 W"}[args.dtype],
         "data": "synthetic",
         "config": {"workload": workload,
+                   "n_rows_total": args.rows if args.scaling == "strong" else world * n_rows,
                    "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
                    "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64"
                                   + (", in-launch over xGMI)" if plan.exchange else ", RCCL)")

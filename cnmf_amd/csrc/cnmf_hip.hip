@@ -4523,8 +4523,18 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G > 0) {
     // one launch of the persistent kernel with n_iter = 1: its in-launch reduction only takes
-    // tickets (no workgroup ever waits), so a plain launch is safe at any residency
+    // tickets (no workgroup ever waits), so a plain launch is safe at any residency.  The layout
+    // is the multi-iteration launch's (wave tiles by default), so the RCCL path and the in-launch
+    // exchange sum the same fp32 partials.
     if (!partials) return set_err(CNMF_ERR_ARG, "null pointer argument");
+    size_t wlds_wt = 0;
+    const int64_t GW = wt_grid(n_rows, false, &wlds_wt);
+    if (GW > 0 && GW <= n_parts) {
+      if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+        return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+      return launch_persistent(G, 1, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB, n_rows,
+                               l1_W, l2_W, l1_H, l2_H, apply_first, 0, hs);
+    }
     if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
       return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
     if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold too few rows");

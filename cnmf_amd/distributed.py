@@ -24,11 +24,19 @@ from .solver import MUPlan, WeightedMUPlan, run_mu
 __all__ = ["shard_bounds", "factorise_sharded"]
 
 
-def shard_bounds(n_rows: int, world: int, rank: int):
-    """Contiguous, balanced [lo, hi) row range of `rank` (the first n_rows % world ranks get +1)."""
-    base, extra = divmod(int(n_rows), int(world))
-    lo = rank * base + min(rank, extra)
-    return lo, lo + base + (1 if rank < extra else 0)
+def shard_bounds(n_rows: int, world: int, rank: int, align: int = 1):
+    """Contiguous, balanced [lo, hi) row range of `rank`.  Rows are dealt in blocks of `align` rows
+    (the first blocks % world ranks get one block more; the last rank also takes the n_rows % align
+    remainder), so with align=64 every shard but possibly the last is a whole number of the
+    persistent kernels' 64-row tiles."""
+    n_rows, world, align = int(n_rows), int(world), max(1, int(align))
+    nb = n_rows // align
+    base, extra = divmod(nb, world)
+    lo = (rank * base + min(rank, extra)) * align
+    hi = lo + (base + (1 if rank < extra else 0)) * align
+    if rank == world - 1:
+        hi = n_rows
+    return lo, hi
 
 
 def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=0.0, l2_reg_W=0.0,

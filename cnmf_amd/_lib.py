@@ -83,6 +83,12 @@ _SIGS = {
     "cnmf_xbuf_free": (_i32, [_vp]),
     "cnmf_xctl_words": (_i64, [_i32]),
     "cnmf_xctl_init": (_i32, [_vp, _vp, _i32, _i32]),
+    "cnmf_init_gram_rows": (_i64, [_i64]),
+    "cnmf_init_gram": (_i32, [_vp, _i32, _i64, _i32, _vp, _i64, _vp]),
+    "cnmf_init_xm": (_i32, [_vp, _i32, _i64, _i32, _i32, _vp, _vp, _vp]),
+    "cnmf_init_stats_rows": (_i64, [_i64]),
+    "cnmf_init_stats": (_i32, [_vp, _i64, _i32, _vp, _i64, _vp]),
+    "cnmf_init_fill": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _f64, _f64, _vp, _i32, _vp]),
     "cnmf_mu_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                         _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp, _i32,
                                         _vp]),

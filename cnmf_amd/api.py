@@ -185,6 +185,33 @@ def _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise):
     return Mw
 
 
+_TORCH_DT = {}  # numpy scalar type -> torch dtype, filled on first use
+GPU_INIT_MIN_ROWS = 65536  # below this the host init costs less than a device round trip
+
+
+def _initial_factors(X, k, init, random_state, device, as_torch, group):
+    """_initialize_nmf (SK:221-373).  The NNDSVD family on a tall X of one process runs its
+    passes over X on the GPU (cnmf_amd.gpu_init, §8 f4); small X, 'random', k > 16 or F > 96, and
+    sharded fits (whose X is one shard of the global matrix) take the host restatement."""
+    torch = _torch()
+    from . import gpu_init as _gpu_init
+    if not _TORCH_DT:
+        _TORCH_DT.update({np.float32: torch.float32, np.float64: torch.float64})
+    n_samples, n_features = X.shape
+    resolved = init
+    if init is None:
+        resolved = "nndsvda" if k <= min(n_samples, n_features) else "random"
+    if (group is None and n_samples >= GPU_INIT_MIN_ROWS and X.min() >= 0
+            and _gpu_init.gpu_init_eligible(n_samples, n_features, k, resolved,
+                                            X.dtype if as_torch else _TORCH_DT.get(X.dtype.type))):
+        dev = torch.device(device) if device is not None else (
+            X.device if as_torch and X.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device()))
+        Xd = (X if as_torch else torch.from_numpy(X)).to(dev).contiguous()
+        return _gpu_init.initialize_nmf_gpu(Xd, k, init=resolved, random_state=random_state)
+    Xh = X if not as_torch else X.detach().to("cpu", torch.float32 if X.dtype == torch.bfloat16 else X.dtype).numpy()
+    return _init.initialize_nmf(Xh, k, init=init, random_state=random_state)
+
+
 def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                    l1_ratio, random_state, verbose, device, group=None, return_plan=False,
                    normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None):
@@ -230,8 +257,7 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
                           "use them as initialization.", RuntimeWarning)
         if k == "auto":
             k = n_features
-        Xh = X if not as_torch else X.detach().to("cpu", torch.float32 if X.dtype == torch.bfloat16 else X.dtype).numpy()
-        W, H = _init.initialize_nmf(Xh, k, init=init, random_state=random_state)
+        W, H = _initial_factors(X, int(k), init, random_state, device, as_torch, group)
     k = int(k)
     if k > 16:
         raise ValueError(f"n_components={k} is not supported: the MI355X kernels handle 1..16.")

@@ -2556,25 +2556,37 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
 //    workgroup and the optional cross-rank exchange are those of mu_iter_sl_kernel.
 // ------------------------------------------------------------------------------------------------
 namespace wt {
-constexpr int F = 81, K = 4, V = F + K;
-constexpr int TSW = 16;                 // samples per wave tile
-constexpr int XBW = TSW * F * 4;        // 5184 B of X per wave tile
-constexpr int NCHW = XBW / 16;          // 324 16-byte chunks
-constexpr int PFW = 6;                  // loads per lane per tile (5 × 64 + 4 chunks)
-constexpr int XSTR = XBW + 16;          // per-wave staging stride (16 zero bytes past each tile)
-constexpr int WBW = TSW * K * 4;        // 256 B of W per wave tile
-constexpr int NQ = 21;                  // features per lane
-constexpr int NACC = NQ * K + K;        // 88 fp32 accumulators per lane (A columns + the B row)
-constexpr int NWV = 4;                  // waves per workgroup
-// LDS carve (bytes): the staging slots and the reduction scratch reuse sl's X / W / P regions; the
-// basis state (L_HT, L_HHT, L_H, L_AB, L_FLAG) sits at sl's offsets so sl_update_basis applies
-constexpr int L_STG = 0;                               // [NWV][XSTR]
-constexpr int L_RED = sl::L_P;                         // [NWV][4 q][NACC] fp32
-constexpr int L_WRES = (sl::L_PTOTAL + 15) / 16 * 16;  // [NWV][nbt_max][16][4] fp32
-static_assert(L_STG + NWV * XSTR <= sl::L_P, "staging slots fit below the scratch");
-static_assert(L_RED + NWV * 4 * NACC * 4 <= sl::L_WN + TS * sl::K * 4, "scratch fits sl's P/WN regions");
-static_assert(NCHW == 5 * 64 + 4, "prefetch layout assumes 324 chunks");
+constexpr int F = 81;
+constexpr int NWV = 4;                  // waves per workgroup (one per SIMD)
 typedef float f2 __attribute__((ext_vector_type(2)));
+
+// geometry of the wave tile for k = KK components: NL = KK lanes per sample (lane l = NL·s + e),
+// TSW = 64 / NL samples per tile, NQ features per lane (e owns [NQ·e, NQ·e + NQ); the lanes past F
+// hold zero-Hᵀ pads)
+template <int KK>
+struct Geo {
+  static constexpr int K = KK, NL = KK, TSW = 64 / KK, V = F + KK, NOUT = KK * V;
+  static constexpr int NQ = (F + KK - 1) / KK;              // 21 (k = 4), 11 (k = 8)
+  static constexpr int XBW = TSW * F * 4;                   // 5184 / 2592 B of X per tile
+  static constexpr int NCHW = XBW / 16;                     // 324 / 162 chunks
+  static constexpr int PFW = (NCHW + 63) / 64;              // 6 / 3 loads per lane
+  static constexpr int LASTL = NCHW - 64 * (PFW - 1);       // lanes of the last load: 4 / 34
+  static constexpr int XSTR = XBW + 16;                     // staging stride (16 zero bytes past)
+  static constexpr int WBW = TSW * KK * 4;                  // 256 B of W per tile
+  static constexpr int NACC = NQ * KK + KK;                 // fp32 accumulators per lane
+  // LDS carve (bytes)
+  static constexpr int L_STG = 0;                                       // [NWV][XSTR]
+  static constexpr int L_WSTG = L_STG + NWV * XSTR;                     // streamed W: [NWV][WBW]
+  static constexpr int L_RED = (L_WSTG + NWV * WBW + 15) / 16 * 16;     // [NWV][NL][NACC] fp32
+  static constexpr int L_H = (L_RED + NWV * NL * NACC * 4 + 15) / 16 * 16;  // H fp64 [K][F]
+  static constexpr int L_AB = L_H + KK * F * 8;                         // AB fp64 [K][V]
+  static constexpr int L_HT = L_AB + NOUT * 8;                          // Hᵀ fp32 [NL·NQ][K]
+  static constexpr int L_HHT = L_HT + NL * NQ * KK * 4;                 // HHᵀ fp64 [K][K]
+  static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 4 ints
+  static constexpr int L_WRES = (L_FLAG + 16 + 15) / 16 * 16;           // [NWV][nbt_max][WBW]
+  static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
+  static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
+};
 
 template <int CTRL>
 __device__ __forceinline__ double dpp64(double v) {
@@ -2587,24 +2599,35 @@ template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// v summed over the 16 lanes l' ≡ l (mod 4) of the wave (all lanes get the sum)
+// lane ^ 4 inside each 8-lane group: row_shr:4 into DPP banks 1 and 3, row_shl:4 into banks 0 and 2
+__device__ __forceinline__ int xor4i(int v) {
+  int r = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xA, false);
+  return __builtin_amdgcn_update_dpp(r, v, 0x104, 0xF, 0x5, false);
+}
+__device__ __forceinline__ double xor4d(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = xor4i((int)(u & 0xFFFFFFFFll)), hi = xor4i((int)(u >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// v summed over the lanes l' ≡ l (mod NL) of the wave (every lane gets its class's sum)
+template <int NL>
 __device__ __forceinline__ float sum_over_samples(float v) {
-  v += dppf<0x124>(v);  // row_ror:4
-  v += dppf<0x128>(v);  // row_ror:8   -> the row's 4 lanes of this q
+  if (NL == 4) v += dppf<0x124>(v);  // row_ror:4
+  v += dppf<0x128>(v);               // row_ror:8
   auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   v = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // + lane ^ 16
   auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);  // + lane ^ 32
 }
 
-// The X prefetch lives in AGPRs and never touches a VGPR: inline-asm loads into AGPR tuples, an
-// asm wait naming them "+a", and asm ds_write_b128 straight from the AGPRs into the staging slot
-// (cdna_hip_programming.md §5.7 item 1, form ii).  Two reasons: (1) hipcc's own counted waits for
-// compiler-issued loads degrade to vmcnt(0) at this loop's header (one tile in flight instead of
-// PD), and (2) under this kernel's VGPR pressure hipcc parks VGPR-resident prefetch registers in
-// AGPRs, copying them before the data has landed.  VMEM returns retire in issue order, so before
-// staging set k, vmcnt(6·(PD-1)) leaves exactly the PD-1 younger sets in flight (compiler-issued
-// memory operations in between only make that wait stricter).
+// The X (and streamed W) prefetch lives in AGPRs and never touches a VGPR: inline-asm loads into
+// AGPR tuples, an asm wait naming them "+a", and asm ds_write_b128 straight from the AGPRs into
+// the staging slot (cdna_hip_programming.md §5.7 item 1, form ii).  Two reasons: (1) hipcc's own
+// counted waits for compiler-issued loads degrade to vmcnt(0) at this loop's header (one tile in
+// flight instead of PD), and (2) under this kernel's VGPR pressure hipcc parks VGPR-resident
+// prefetch registers in AGPRs, copying them before the data has landed.  VMEM operations retire
+// in issue order, so before staging set k, vmcnt(L·(PD-1)) (L loads per set) leaves exactly the
+// PD-1 younger sets in flight; compiler-issued memory operations in between only make it stricter.
 #ifdef CNMF_X_PLAIN
 #define WT_LD "global_load_dwordx4 %0, %1, off"
 #else
@@ -2614,47 +2637,235 @@ __device__ __forceinline__ void ld16(u32x4& r, const unsigned char* p) {
   asm volatile(WT_LD : "=a"(r) : "v"(p) : "memory");
 }
 template <int N>
-__device__ __forceinline__ void wait_set(u32x4 (&pf)[PFW]) {
-  asm volatile("s_waitcnt vmcnt(%6)"
-               : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5])
-               : "n"(N)
-               : "memory");
+__device__ __forceinline__ void wait_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-// the tile's 16-byte chunks of this lane: l + 64u (u < 5), and 320 + l for lanes 0-3 (others re-load
-// chunk l: not staged; every lane issues the same six loads)
-__device__ __forceinline__ void prefetch(u32x4 (&pf)[PFW], const unsigned char* __restrict__ X, int64_t tile, int l) {
-#ifdef CNMF_DIAG_L2
-  const unsigned char* xs = X + (size_t)(tile & 255) * XBW + 16 * l;
-#else
-  const unsigned char* xs = X + (size_t)tile * XBW + 16 * l;
-#endif
-#pragma unroll
-  for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
-  ld16(pf[PFW - 1], l < 4 ? xs + 1024 * (PFW - 1) : xs);
+template <int N, int C>
+__device__ __forceinline__ void wait_set(u32x4 (&pf)[C]) {
+  if constexpr (C == 7)
+    asm volatile("s_waitcnt vmcnt(%7)"
+                 : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5]), "+a"(pf[6])
+                 : "n"(N) : "memory");
+  else if constexpr (C == 6)
+    asm volatile("s_waitcnt vmcnt(%6)"
+                 : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5])
+                 : "n"(N) : "memory");
+  else if constexpr (C == 4)
+    asm volatile("s_waitcnt vmcnt(%4)" : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]) : "n"(N) : "memory");
+  else if constexpr (C == 3)
+    asm volatile("s_waitcnt vmcnt(%3)" : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]) : "n"(N) : "memory");
+  else
+    static_assert(C == 3 || C == 4 || C == 6 || C == 7, "prefetch set size");
 }
 template <int OFF>
 __device__ __forceinline__ void st16(unsigned addr, const u32x4& v) {
   asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
 }
-__device__ __forceinline__ void stage(unsigned char* stg, const u32x4 (&pf)[PFW], int l) {
-  const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
-  st16<0>(addr, pf[0]);
-  st16<1024>(addr, pf[1]);
-  st16<2048>(addr, pf[2]);
-  st16<3072>(addr, pf[3]);
-  st16<4096>(addr, pf[4]);
-  if (l < 4) st16<5120>(addr, pf[5]);
+template <int OFF, int U>
+__device__ __forceinline__ void stage_rec(unsigned addr, const u32x4* pf) {
+  st16<OFF>(addr, pf[0]);
+  if constexpr (U > 1) stage_rec<OFF + 1024, U - 1>(addr, pf + 1);
 }
 }  // namespace wt
 
-template <int PD, bool MULTI = false>
+// sum of `cnt` rows (m0, m0 + step, ...) of NOUT doubles each, in row order, sc1 loads (the NOUT-
+// generic form of sum_rows_sc1: up to three outputs per thread, their row batches in flight together)
+template <int NOUT>
+__device__ __forceinline__ void sum_rows_n(const double* rows, int m0, int step, int cnt, double* lds_out,
+                                           double* g_out, int t) {
+  constexpr int U = (NOUT + NT - 1) / NT;
+  constexpr int RB = U == 1 ? 16 : (U == 2 ? 16 : 8);
+  int o[U];
+  double v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    o[u] = t + NT * u < NOUT ? t + NT * u : t;
+    v[u] = 0.0;
+  }
+  for (int m = 0; m < cnt; m += RB) {
+    double x[RB][U];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+      const int row = m0 + min(m + r, cnt - 1) * step;
+#pragma unroll
+      for (int u = 0; u < U; ++u) x[r][u] = ld_sc1(rows + (size_t)row * NOUT + o[u]);
+    }
+#pragma unroll
+    for (int r = 0; r < RB; ++r)
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] += m + r < cnt ? x[r][u] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (t + NT * u < NOUT) {
+      if (lds_out) lds_out[o[u]] = v[u];
+      st_sc1(g_out + o[u], v[u]);
+    }
+}
+
+// the cross-rank all-reduce of AB inside a persistent launch (xchg_allreduce_ab's protocol,
+// generic in the accumulator count NOUT; slot stride 2·NOUT words)
+template <int NOUT>
+__device__ __forceinline__ void xchg_allreduce_n(uint64_t* xctl, double* AB, double* sAB, uint32_t* err, int it, int t) {
+  constexpr int U = (NOUT + NT - 1) / NT;
+  const int xrank = (int)__hip_atomic_load(xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int xworld = (int)__hip_atomic_load(xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t gen =
+      (uint32_t)__hip_atomic_load(xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (uint32_t)it + 1u;
+  auto peer = [&](int r) {
+    return reinterpret_cast<uint64_t*>(__hip_atomic_load(xctl + XC_PEERS + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  TL_X(it, 0);
+  const size_t slot = 2 * (size_t)NOUT;
+  const size_t par = (size_t)(gen & 1u) * xworld * slot;
+  int o[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) o[u] = t + NT * u < NOUT ? t + NT * u : t;
+  {
+    const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    const uint64_t tag = (uint64_t)(bad ? sl::XPOISON : gen) << 32;
+    for (int pr = 0; pr < xworld; ++pr) {
+      uint64_t* dst = peer(pr) + par + (size_t)xrank * slot;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (t + NT * u < NOUT) {
+          const uint64_t bv = (uint64_t)__double_as_longlong(sAB[o[u]]);
+          __hip_atomic_store(dst + 2 * o[u], tag | (bv & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dst + 2 * o[u] + 1, tag | (bv >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+  }
+  TL_X(it, 1);
+  const uint64_t* mine = peer(xrank) + par;
+  double v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = 0.0;
+  constexpr int QB = 4;  // ranks polled per round (their loads in flight together)
+  for (int q0 = 0; q0 < xworld; q0 += QB) {
+    uint64_t w[QB][2 * U];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+#pragma unroll
+      for (int j = 0; j < QB; ++j) {
+        const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          w[j][2 * u] = __hip_atomic_load(src + 2 * o[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          w[j][2 * u + 1] = __hip_atomic_load(src + 2 * o[u] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      bool ok = true, poison = false;
+#pragma unroll
+      for (int j = 0; j < QB; ++j)
+#pragma unroll
+        for (int m = 0; m < 2 * U; ++m) {
+          const uint32_t tg = (uint32_t)(w[j][m] >> 32);
+          ok = ok && tg == gen;
+          poison = poison || tg == sl::XPOISON;
+        }
+      if (ok) break;
+      if (poison) {
+        __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+        __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int j = 0; j < QB; ++j)
+      if (q0 + j < xworld)  // rank order
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          v[u] += __longlong_as_double((long long)((w[j][2 * u + 1] << 32) | (w[j][2 * u] & 0xFFFFFFFFull)));
+  }
+  TL_X(it, 2);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (t + NT * u < NOUT) {
+      sAB[o[u]] = v[u];
+      st_sc1(AB + o[u], v[u]);
+    }
+  TL_X(it, 3);
+}
+
+// Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) and HHᵀ (fp64; lanes over f, fixed shuffle
+// tree) from the fp64 H in LDS — sl_derive_basis for k = KK
+template <int KK>
+__device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
+  using G = wt::Geo<KK>;
+  const double* sH = reinterpret_cast<const double*>(smem + G::L_H);
+  float* sHt = reinterpret_cast<float*>(smem + G::L_HT);
+  double* sHHt = reinterpret_cast<double*>(smem + G::L_HHT);
+  for (int e = t; e < G::NL * G::NQ * KK; e += NT) {
+    const int f = e / KK;
+    const int j = e - f * KK;
+    sHt[e] = f < wt::F ? (float)sH[j * wt::F + f] : 0.f;
+  }
+  const int lane = t & 63;
+  const int wave = t >> 6;
+  for (int e = wave; e < KK * KK; e += NWAVE) {
+    const int j = e / KK;
+    const int m = e - j * KK;
+    double v = 0.0;
+    for (int f = lane; f < wt::F; f += 64) v = fma(sH[j * wt::F + f], sH[m * wt::F + f], v);
+    v = wave_sum(v);
+    if (lane == 0) sHHt[e] = v;
+  }
+  __syncthreads();
+}
+// H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728) —
+// sl_update_basis for k = KK
+template <int KK>
+__device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, double l1, double l2) {
+  using G = wt::Geo<KK>;
+  constexpr int KF = KK * wt::F;
+  constexpr int U = (KF + NT - 1) / NT;
+  double* sH = reinterpret_cast<double*>(smem + G::L_H);
+  const double* sAB = reinterpret_cast<const double*>(smem + G::L_AB);
+  double hn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + NT * u;
+    hn[u] = 0.0;
+    if (e < KF) {
+      const int j = e / wt::F;
+      const int f = e - j * wt::F;
+      const double h = sH[e];
+      const double num = sAB[j * G::V + f];                                      // (WᵀX)[j][f], SK:639
+      double den = 0.0;                                                          // ((WᵀW)·H)[j][f], SK:640
+      for (int m = 0; m < KK; ++m) den = fma(sAB[j * G::V + wt::F + m], sH[m * wt::F + f], den);
+      if (l1 > 0.0) den += l1;                                                   // SK:702-703
+      if (l2 > 0.0) den = den + l2 * h;                                          // SK:704-705
+      if (den == 0.0) den = EPS32;                                               // SK:706
+      hn[u] = h * (num / den);                                                   // SK:722-726
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (t + NT * u < KF) sH[t + NT * u] = hn[u];
+  __syncthreads();
+  wt_derive_basis<KK>(smem, t);
+}
+
+template <int KK, bool WRES, int PD, bool MULTI = false>
 __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   using namespace wt;
+  using G_ = Geo<KK>;
+  constexpr int NL = G_::NL, TSW = G_::TSW, NQ = G_::NQ, V = G_::V, NOUT = G_::NOUT;
+  constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, NACC = G_::NACC;
+  constexpr int PFW = G_::PFW, LASTL = G_::LASTL;
+  constexpr int PFS = PFW + (WRES ? 0 : 1);  // loads per prefetch set (+ the W tile when streamed)
+  constexpr int KP = KK / 2;                 // component pairs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
   const int l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int s = l >> 2, q = l & 3;
+  const int s = l / NL, e = l % NL;
   const int b = blockIdx.x;
   const int G = gridDim.x;
   const int NW = NWV * G;
@@ -2663,77 +2874,110 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   const int g = b % NG;
   const int gs = (G - g + NG - 1) / NG;
   const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
-  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);     // this wave's tiles per iteration
+  unsigned char* Wb = reinterpret_cast<unsigned char*>(a.W);
+  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);  // this wave's tiles per iteration
   const int nbt_max = (int)((a.n_tiles + NW - 1) / NW);
-  unsigned char* stg = smem + L_STG + w * XSTR;
-  float* wres = reinterpret_cast<float*>(smem + L_WRES + (size_t)w * nbt_max * WBW);  // [i][16][4]
-  float* red = reinterpret_cast<float*>(smem + L_RED);
-  double* sH = reinterpret_cast<double*>(smem + sl::L_H);
-  double* sAB = reinterpret_cast<double*>(smem + sl::L_AB);
-  int* sFlag = reinterpret_cast<int*>(smem + sl::L_FLAG);
+  unsigned char* stg = smem + G_::L_STG + w * XSTR;
+  unsigned char* wstg = smem + G_::L_WSTG + w * WBW;  // streamed W: this wave's current tile
+  float* wres = reinterpret_cast<float*>(smem + G_::L_WRES + (size_t)w * nbt_max * WBW);  // [i][TSW][K]
+  float* red = reinterpret_cast<float*>(smem + G_::L_RED);
+  double* sH = reinterpret_cast<double*>(smem + G_::L_H);
+  double* sAB = reinterpret_cast<double*>(smem + G_::L_AB);
+  int* sFlag = reinterpret_cast<int*>(smem + G_::L_FLAG);
   uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
   uint32_t* cnt_top = a.cnt + CNT_TOP;
   uint32_t* flag = a.cnt + CNT_FLAG;
   uint32_t* err = a.cnt + CNT_ERR;
 
-  // ---- the basis for the first iteration, the staging pads, this wave's W tiles
-  for (int e = t; e < K * F; e += NT) sH[e] = a.H64[e];
+  // ---- the basis for the first iteration, the staging pads, this wave's W tiles (W resident)
+  for (int i = t; i < KK * F; i += NT) sH[i] = a.H64[i];
   if (a.apply_first)
-    for (int e = t; e < K * V; e += NT) sAB[e] = a.AB[e];
+    for (int i = t; i < NOUT; i += NT) sAB[i] = a.AB[i];
   if (l < 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
-  for (int c = l; c < nbt * (WBW / 16); c += 64) {
-    const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
-    *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
-        *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(a.W) + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
-  }
+  if (WRES)
+    for (int c = l; c < nbt * (WBW / 16); c += 64) {
+      const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
+          *reinterpret_cast<const u32x4*>(Wb + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
+    }
   __syncthreads();
   if (a.apply_first)
-    sl_update_basis(smem, t, a.l1H, a.l2H);
+    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
   else
-    sl_derive_basis(smem, t);
+    wt_derive_basis<KK>(smem, t);
 
-  // the lane's Hᵀ (fp32 pairs: components 0,1 and 2,3 of each of its features) and HHᵀ row q
-  f2 h01[NQ], h23[NQ];
-  double hh[K];
+  // the lane's Hᵀ (fp32 component pairs of each of its NQ features) and HHᵀ row e
+  f2 hp[NQ][KP];
+  double hh[KK];
   auto load_basis = [&]() {
-    const float* sHt = reinterpret_cast<const float*>(smem + sl::L_HT);
-    const double* sHHt = reinterpret_cast<const double*>(smem + sl::L_HHT);
+    const float* sHt = reinterpret_cast<const float*>(smem + G_::L_HT);
+    const double* sHHt = reinterpret_cast<const double*>(smem + G_::L_HHT);
 #pragma unroll
-    for (int c = 0; c < NQ; ++c) {
-      const float4 h = *reinterpret_cast<const float4*>(sHt + (NQ * q + c) * K);
-      h01[c] = f2{h.x, h.y};
-      h23[c] = f2{h.z, h.w};
-    }
+    for (int c = 0; c < NQ; ++c)
 #pragma unroll
-    for (int m = 0; m < K; ++m) hh[m] = sHHt[q * K + m];
+      for (int p4 = 0; p4 < KK / 4; ++p4) {
+        const float4 h = *reinterpret_cast<const float4*>(sHt + (NQ * e + c) * KK + 4 * p4);
+        hp[c][2 * p4] = f2{h.x, h.y};
+        hp[c][2 * p4 + 1] = f2{h.z, h.w};
+      }
+#pragma unroll
+    for (int m = 0; m < KK; ++m) hh[m] = sHHt[e * KK + m];
   };
   load_basis();
 
-  f2 acc01[NQ], acc23[NQ], accB01, accB23;
+  f2 acc[NQ][KP], accB[KP];
   auto zero_acc = [&]() {
 #pragma unroll
-    for (int c = 0; c < NQ; ++c) acc01[c] = acc23[c] = f2{0.f, 0.f};
-    accB01 = accB23 = f2{0.f, 0.f};
+    for (int c = 0; c < NQ; ++c)
+#pragma unroll
+      for (int p = 0; p < KP; ++p) acc[c][p] = f2{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < KP; ++p) accB[p] = f2{0.f, 0.f};
   };
   zero_acc();
 
-  const int total = a.n_iter * nbt;
-  u32x4 pf[PD][PFW];
+  // the tile's 16-byte chunks of this lane: l + 64u (u < PFW - 1) and, for lanes < LASTL, the last
+  // (other lanes re-load chunk l: never staged; every lane issues the same loads), then the W tile
+  // when streamed (lanes < 16; others re-load chunk l)
+  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile) {
+#ifdef CNMF_DIAG_L2
+    const unsigned char* xs = Xb + (size_t)(tile & 255) * XBW + 16 * l;
+#else
+    const unsigned char* xs = Xb + (size_t)tile * XBW + 16 * l;
+#endif
 #pragma unroll
-  for (int k = 0; k < PD; ++k) prefetch(pf[k], Xb, gw + (int64_t)NW * k, l);  // the host keeps nbt > PD
+    for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
+    ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
+    if (!WRES) ld16(pf[PFW], l < WBW / 16 ? Wb + (size_t)tile * WBW + 16 * l : xs);
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS]) {
+    const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
+    stage_rec<0, PFW - 1>(addr, pf);
+    if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
+    if (!WRES && l < WBW / 16) st16<0>((unsigned)(uintptr_t)(wstg + 16 * l), pf[PFW]);
+  };
+
+  const int total = a.n_iter * nbt;
+  u32x4 pf[PD][PFS];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+  // W streamed: a tile's W store (body x) must have retired before its next load is issued (the
+  // prefetch at step x + nbt - PD); the step waits retire every operation older than the set they
+  // wait for, which covers that store when nbt >= 2·PD + 1 (the host guarantees it)
   TL_START;
 
   bool alive = true;
   // position counters (wave-uniform, incremental: no division per tile): the tile being processed
-  // (iteration cur_it, index cur_i) and the next one to prefetch (nx_i)
+  // (iteration cur_it, index cur_i) and the next one to prefetch (nx_i).  Every step stages its
+  // register set and re-issues it unconditionally (past the launch's last position: the wave's
+  // first tile again, never used), so the count of younger loads is the same on every path.
   int cur_i = 0, cur_it = 0, nx_i = PD;
-  // Every step stages its register set and re-issues it unconditionally (past the launch's last
-  // position: the wave's first tile again, never used), so that the count of younger loads is the
-  // same on every path: staging set k waits vmcnt(6·(PD-1)), i.e. PD tiles stay in flight.
-  auto step = [&](u32x4 (&pfk)[PFW]) {
-    wait_set<PFW * (PD - 1)>(pfk);
-    stage(stg, pfk, l);
-    prefetch(pfk, Xb, gw + (int64_t)NW * nx_i, l);
+  auto step = [&](u32x4 (&pfk)[PFS]) {
+    // younger than this set's loads: the PD-1 later sets and, with W streamed, the W stores of the
+    // PD bodies since (one each)
+    wait_set<PFS * (PD - 1) + (WRES ? 0 : PD), PFS>(pfk);
+    stage(pfk);
+    prefetch(pfk, gw + (int64_t)NW * nx_i);
     if (++nx_i == nbt) nx_i = 0;
   };
   auto body = [&]() {
@@ -2743,89 +2987,135 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       ++cur_it;
     }
     const bool last_it = it + 1 == a.n_iter;
-    // phase 1: x along the lane's row, packed fp32 chains of 7 folded into fp64
-    const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * q;
+    const int64_t tile = gw + (int64_t)NW * i;
+    // phase 1: x along the lane's row, packed fp32 chains of 7 features folded into fp64
+    const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * e;
     float xv[NQ];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) xv[c] = xr[c];
-    double p0, p1, p2, p3;
+    double p[KK];
 #pragma unroll
     for (int c0 = 0; c0 < NQ; c0 += 7) {
-      f2 c01 = f2{0.f, 0.f}, c23 = f2{0.f, 0.f};
+      f2 ch[KP];
 #pragma unroll
-      for (int c = c0; c < c0 + 7; ++c) {
+      for (int q = 0; q < KP; ++q) ch[q] = f2{0.f, 0.f};
+#pragma unroll
+      for (int c = c0; c < (c0 + 7 < NQ ? c0 + 7 : NQ); ++c) {
         const f2 xx = f2{xv[c], xv[c]};
-        c01 = __builtin_elementwise_fma(xx, h01[c], c01);
-        c23 = __builtin_elementwise_fma(xx, h23[c], c23);
+#pragma unroll
+        for (int q = 0; q < KP; ++q) ch[q] = __builtin_elementwise_fma(xx, hp[c][q], ch[q]);
       }
-      if (c0 == 0) {
-        p0 = (double)c01.x; p1 = (double)c01.y; p2 = (double)c23.x; p3 = (double)c23.y;
-      } else {
-        p0 += (double)c01.x; p1 += (double)c01.y; p2 += (double)c23.x; p3 += (double)c23.y;
+#pragma unroll
+      for (int q = 0; q < KP; ++q) {
+        if (c0 == 0) {
+          p[2 * q] = (double)ch[q].x;
+          p[2 * q + 1] = (double)ch[q].y;
+        } else {
+          p[2 * q] += (double)ch[q].x;
+          p[2 * q + 1] += (double)ch[q].y;
+        }
       }
     }
-    // quad reduce-scatter: lane q ends with num[s][q] (fp64)
-    const bool hi2 = (q & 2) != 0, hi1 = (q & 1) != 0;
-    double k0 = hi2 ? p2 : p0, k1 = hi2 ? p3 : p1;
-    const double s0 = hi2 ? p0 : p2, s1 = hi2 ? p1 : p3;
-    k0 += dpp64<0x4E>(s0);  // quad_perm [2,3,0,1]
-    k1 += dpp64<0x4E>(s1);
-    const double kk = hi1 ? k1 : k0, ss = hi1 ? k0 : k1;
-    const double num = kk + dpp64<0xB1>(ss);  // quad_perm [1,0,3,2]
-    // phase 2: w[s][q] <- w·num/den (SK:553-629) against the resident W
-    float* wt_ = wres + i * (TSW * K);
-    const float4 wv = *reinterpret_cast<const float4*>(wt_ + s * K);
-    const float wq = hi2 ? (hi1 ? wv.w : wv.z) : (hi1 ? wv.y : wv.x);
-    const double wold = (double)wq;
+    // reduce-scatter over the NL lanes of the sample: lane e ends with num[s][e] (fp64)
+    double num;
+    {
+      const bool b1 = (e & 1) != 0, b2 = (e & 2) != 0;
+      double k2[2];
+      if constexpr (KK == 8) {
+        const bool b4 = (e & 4) != 0;
+        double k4[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const double keep = b4 ? p[4 + m] : p[m], send = b4 ? p[m] : p[4 + m];
+          k4[m] = keep + xor4d(send);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const double keep = b2 ? k4[2 + m] : k4[m], send = b2 ? k4[m] : k4[2 + m];
+          k2[m] = keep + dpp64<0x4E>(send);  // quad_perm [2,3,0,1]
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const double keep = b2 ? p[2 + m] : p[m], send = b2 ? p[m] : p[2 + m];
+          k2[m] = keep + dpp64<0x4E>(send);
+        }
+      }
+      const double keep = b1 ? k2[1] : k2[0], send = b1 ? k2[0] : k2[1];
+      num = keep + dpp64<0xB1>(send);  // quad_perm [1,0,3,2]
+    }
+    // phase 2: w[s][e] <- w·num/den (SK:553-629)
+    float* wt_ = WRES ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);
+    float wv[KK];
+#pragma unroll
+    for (int m4 = 0; m4 < KK / 4; ++m4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(wt_ + s * KK + 4 * m4);
+      wv[4 * m4] = v4.x;
+      wv[4 * m4 + 1] = v4.y;
+      wv[4 * m4 + 2] = v4.z;
+      wv[4 * m4 + 3] = v4.w;
+    }
+    const double wold = (double)wt_[s * KK + e];
     double den = 0.0;
-    den = fma((double)wv.x, hh[0], den);
-    den = fma((double)wv.y, hh[1], den);
-    den = fma((double)wv.z, hh[2], den);
-    den = fma((double)wv.w, hh[3], den);
+#pragma unroll
+    for (int m = 0; m < KK; ++m) den = fma((double)wv[m], hh[m], den);
     if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
     if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
     if (den == 0.0) den = EPS32;                // SK:620
     const float wn = (float)(wold * (num / den));  // SK:622-629
-    wt_[s * K + q] = wn;
-    const f2 w01 = f2{dppf<0x00>(wn), dppf<0x55>(wn)};  // quad broadcasts of lanes 0, 1
-    const f2 w23 = f2{dppf<0xAA>(wn), dppf<0xFF>(wn)};  // ... and 2, 3
-    // phase 3: A[·][f] += w'·x[f], B[q][·] += w'_q·w' (fp32 per lane over the iteration)
+    wt_[s * KK + e] = wn;
+    if (!WRES) reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wn;  // lane l = (s, e)
+    // w'[s][·]: the sample's row back from LDS (this wave's writes above precede the reads)
+    f2 wp[KP];
+#pragma unroll
+    for (int m4 = 0; m4 < KK / 4; ++m4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(wt_ + s * KK + 4 * m4);
+      wp[2 * m4] = f2{v4.x, v4.y};
+      wp[2 * m4 + 1] = f2{v4.z, v4.w};
+    }
+    // phase 3: A[·][f] += w'·x[f], B[e][·] += w'_e·w' (fp32 per lane over the iteration)
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
       const f2 xx = f2{xv[c], xv[c]};
-      acc01[c] = __builtin_elementwise_fma(xx, w01, acc01[c]);
-      acc23[c] = __builtin_elementwise_fma(xx, w23, acc23[c]);
+#pragma unroll
+      for (int q = 0; q < KP; ++q) acc[c][q] = __builtin_elementwise_fma(xx, wp[q], acc[c][q]);
     }
-    accB01 = __builtin_elementwise_fma(f2{wn, wn}, w01, accB01);
-    accB23 = __builtin_elementwise_fma(f2{wn, wn}, w23, accB23);
+#pragma unroll
+    for (int q = 0; q < KP; ++q) accB[q] = __builtin_elementwise_fma(f2{wn, wn}, wp[q], accB[q]);
     if (i + 1 != nbt) return;
 
-    // ---- end of this wave's iteration: its sums over the 16 sample lanes of each q -> LDS
+    // ---- end of this wave's iteration: its sums over the sample lanes of each e -> LDS
     {
-      float* rw = red + (w * 4 + q) * NACC;
+      float* rw = red + (w * NL + e) * NACC;
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) {
-        const float4 v = make_float4(sum_over_samples(acc01[c].x), sum_over_samples(acc01[c].y),
-                                     sum_over_samples(acc23[c].x), sum_over_samples(acc23[c].y));
-        if (l < 4) *reinterpret_cast<float4*>(rw + c * K) = v;
+      for (int c = 0; c < NQ; ++c)
+#pragma unroll
+        for (int q2 = 0; q2 < KP; q2 += 2) {
+          const float4 v = make_float4(sum_over_samples<NL>(acc[c][q2].x), sum_over_samples<NL>(acc[c][q2].y),
+                                       sum_over_samples<NL>(acc[c][q2 + 1].x), sum_over_samples<NL>(acc[c][q2 + 1].y));
+          if (l < NL) *reinterpret_cast<float4*>(rw + c * KK + 2 * q2) = v;
+        }
+#pragma unroll
+      for (int q2 = 0; q2 < KP; q2 += 2) {
+        const float4 v = make_float4(sum_over_samples<NL>(accB[q2].x), sum_over_samples<NL>(accB[q2].y),
+                                     sum_over_samples<NL>(accB[q2 + 1].x), sum_over_samples<NL>(accB[q2 + 1].y));
+        if (l < NL) *reinterpret_cast<float4*>(rw + NQ * KK + 2 * q2) = v;
       }
-      const float4 v = make_float4(sum_over_samples(accB01.x), sum_over_samples(accB01.y),
-                                   sum_over_samples(accB23.x), sum_over_samples(accB23.y));
-      if (l < 4) *reinterpret_cast<float4*>(rw + NQ * K) = v;
     }
     zero_acc();
     __syncthreads();
     // the workgroup's fp64 row [K][V]: the four waves' sums in wave order (deterministic)
     {
-      double* prow = a.partials + (size_t)b * (K * V);
-      for (int e = t; e < K * V; e += NT) {
-        const int j = e / V;
-        const int v = e - j * V;
-        const int qq = v < F ? v / NQ : j;
-        const int idx = v < F ? (v - NQ * qq) * K + j : NQ * K + (v - F);
-        const float* rr = red + qq * NACC + idx;
-        const double val = ((double)rr[0] + (double)rr[4 * NACC]) + ((double)rr[8 * NACC] + (double)rr[12 * NACC]);
-        __hip_atomic_store(prow + e, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double* prow = a.partials + (size_t)b * NOUT;
+      for (int o = t; o < NOUT; o += NT) {
+        const int j = o / V;
+        const int v = o - j * V;
+        const int ee = v < F ? v / NQ : j;
+        const int idx = v < F ? (v - NQ * ee) * KK + j : NQ * KK + (v - F);
+        const float* rr = red + ee * NACC + idx;
+        constexpr int WS = NL * NACC;  // wave stride
+        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
@@ -2839,7 +3129,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     __syncthreads();
     if (sFlag[0]) {  // group combiner
-      sum_rows_sc1(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * (K * V), t);
+      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -2848,8 +3138,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
-        sum_rows_sc1(a.groups, 0, 1, NG, sAB, a.AB, t);
-        if (MULTI) xchg_allreduce_ab(a.xctl, a.AB, sAB, err, it, t);
+        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AB, sAB, err, it, t);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0 && !last_it)
@@ -2860,22 +3150,22 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     const bool top = sFlag[1] != 0;
     if (last_it) {
       alive = false;
-      // this wave's W back to HBM, once per launch
-      for (int c = l; c < nbt * (WBW / 16); c += 64) {
-        const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(a.W) + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
-            *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
-      }
+      if (WRES)  // this wave's W back to HBM, once per launch
+        for (int c = l; c < nbt * (WBW / 16); c += 64) {
+          const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+          *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+              *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
+        }
       if (!top) return;
       // the last combiner of the launch: every other workgroup has arrived for the last time
-      if (a.apply_last) sl_update_basis(smem, t, a.l1H, a.l2H);
-      for (int e = t; e < K * F; e += NT) a.H64[e] = sH[e];
-      for (int e = t; e < F * K; e += NT) {
-        const int f = e / K;
-        const int j = e - f * K;
-        a.Ht[e] = sH[j * F + f];
+      if (a.apply_last) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < F * KK; o += NT) {
+        const int f = o / KK;
+        const int j = o - f * KK;
+        a.Ht[o] = sH[j * F + f];
       }
-      if (t < K * K) a.HHt[t] = reinterpret_cast<const double*>(smem + sl::L_HHT)[t];
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2907,10 +3197,10 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
         alive = false;
         return;
       }
-      for (int e = t; e < K * V; e += NT) sAB[e] = ld_sc1(a.AB + e);
+      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
     }
-    sl_update_basis(smem, t, a.l1H, a.l2H);
+    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
     load_basis();
     TL(it, 1);
   };
@@ -3548,6 +3838,190 @@ static size_t reduce_lds(int n_out, int fuse, int F, int k) {
   size_t d = RED_NT + 2;
   if (fuse) d += ((size_t)(n_out + 1) & ~size_t(1)) + update_lds_doubles(F, k, padded_k(k));
   return d * sizeof(double);
+}
+
+// ------------------------------------------------------------------------------------------------
+// GPU NNDSVD initialisation (sklearn's _initialize_nmf SK:317-373 over
+// randomized_svd, extmath.py:530-604).  sklearn's range finder alternates Q <- lu(X·Q),
+// Q <- lu(Xᵀ·Q): only span(Q) matters to the result (U, s, Vt are invariant under an orthonormal
+// change of basis of the range; svd_flip fixes the signs), and span(Xᵀ·X·Q) needs only the F × F
+// Gram matrix C = XᵀX.  So the device does the work that scales with N:
+//   ig_gram_kernel    C = XᵀX and the column sums of X (fp64, per-workgroup partial rows, reduced by
+//                     cnmf_reduce_partials) — one pass over X;
+//   ig_xm_kernel      U = X·M (M = F × k from the small host algebra), fp64 — one pass over X;
+//   ig_stats_kernel   per column of U: Σ max(u,0)², Σ min(u,0)², and the first entry of largest |u|
+//                     (svd_flip's u-based sign) — per-workgroup rows;
+//   ig_fill_kernel    W from U: sqrt(S0)|u| (j = 0) or lbd·part(sign·u)/‖part‖, < eps -> 0, and the
+//                     nndsvda fill — in X's dtype;
+// while the host does sklearn's F × r / r × r algebra in fp64 (cnmf_amd/gpu_init.py).
+// ------------------------------------------------------------------------------------------------
+namespace ig {
+constexpr int FP = 96;   // features padded (F <= 96)
+constexpr int GT = 64;   // rows per staged tile
+constexpr int KMAX = 16;
+}  // namespace ig
+
+// C = XᵀX (F × F) and colsum (F) of this workgroup's rows [r0, r1): thread (a, c) owns C rows
+// 3a..3a+2 × columns 12c..12c+11 (fp64 registers); the tile is staged in LDS as fp64 [GT][FP].
+// Output row: [F·F | F].
+template <typename TX>
+__global__ __launch_bounds__(256) void ig_gram_kernel(const TX* __restrict__ X, int64_t n_rows, int F,
+                                                      int64_t rows_per_block, double* __restrict__ partials) {
+  using namespace ig;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* tile = reinterpret_cast<double*>(smem);  // [GT][FP]
+  const int t = threadIdx.x;
+  const int a = t >> 3, c = t & 7;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n_rows ? r0 + rows_per_block : n_rows;
+  double acc[3][12], cs[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cs[i] = 0.0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) acc[i][j] = 0.0;
+  }
+  for (int64_t rt = r0; rt < r1; rt += GT) {
+    const int nr = (int)(r1 - rt < GT ? r1 - rt : GT);
+    __syncthreads();
+    for (int e = t; e < GT * FP; e += 256) {
+      const int r = e / FP, f = e - r * FP;
+      tile[e] = (r < nr && f < F) ? (double)to_c(*(X + (rt + r) * F + f)) : 0.0;
+    }
+    __syncthreads();
+    for (int r = 0; r < nr; ++r) {
+      const double* row = tile + r * FP;
+      double xa[3], xb[12];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) xa[i] = row[3 * a + i];
+#pragma unroll
+      for (int j = 0; j < 12; ++j) xb[j] = row[12 * c + j];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 12; ++j) acc[i][j] = fma(xa[i], xb[j], acc[i][j]);
+        cs[i] += xa[i];
+      }
+    }
+  }
+  double* prow = partials + (size_t)blockIdx.x * (F * F + F);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int fi = 3 * a + i;
+    if (fi >= F) continue;
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int fj = 12 * c + j;
+      if (fj < F) prow[fi * F + fj] = acc[i][j];
+    }
+    if (c == 0) prow[F * F + fi] = cs[i];
+  }
+}
+
+// U[n][j] = Σ_f X[n][f]·M[f][j] (fp64), k <= 16: thread = (row of the tile, component group)
+template <typename TX>
+__global__ __launch_bounds__(256) void ig_xm_kernel(const TX* __restrict__ X, int64_t n_rows, int F, int k,
+                                                    const double* __restrict__ M, double* __restrict__ U) {
+  using namespace ig;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* sM = reinterpret_cast<double*>(smem);  // [F][k]
+  float* tile = reinterpret_cast<float*>(smem + (size_t)FP * KMAX * 8);  // [GT][F + 1] (fp32 copy; exact for f32/bf16)
+  double* tile64 = reinterpret_cast<double*>(smem + (size_t)FP * KMAX * 8);  // f64 X: [GT][F + 1]
+  const int t = threadIdx.x;
+  for (int e = t; e < F * k; e += 256) sM[e] = M[e];
+  const int r = t & (GT - 1), jg = t >> 6;  // 4 component groups: j = jg, jg + 4, ...
+  const int64_t n_tiles = (n_rows + GT - 1) / GT;
+  for (int64_t tb = blockIdx.x; tb < n_tiles; tb += gridDim.x) {
+    const int64_t row0 = tb * GT;
+    const int nr = (int)(n_rows - row0 < GT ? n_rows - row0 : GT);
+    __syncthreads();
+    for (int e = t; e < nr * F; e += 256) {
+      const int rr = e / F, f = e - rr * F;
+      if (std::is_same<TX, double>::value)
+        tile64[rr * (F + 1) + f] = (double)to_c(*(X + row0 * F + e));
+      else
+        tile[rr * (F + 1) + f] = (float)to_c(*(X + row0 * F + e));
+    }
+    __syncthreads();
+    if (r < nr) {
+      for (int j = jg; j < k; j += 4) {
+        double u = 0.0;
+        for (int f = 0; f < F; ++f) {
+          const double x = std::is_same<TX, double>::value ? tile64[r * (F + 1) + f] : (double)tile[r * (F + 1) + f];
+          u = fma(x, sM[f * k + j], u);
+        }
+        U[(row0 + r) * k + j] = u;
+      }
+    }
+  }
+}
+
+// per column j of U (N × k fp64) over this workgroup's rows: [Σ max(u,0)², Σ min(u,0)², max|u|,
+// the u at the first row attaining it, that row] — 5 doubles per column
+__global__ __launch_bounds__(256) void ig_stats_kernel(const double* __restrict__ U, int64_t n_rows, int k,
+                                                       int64_t rows_per_block, double* __restrict__ out) {
+  __shared__ double red[256][5];
+  const int t = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < n_rows ? r0 + rows_per_block : n_rows;
+  for (int j = 0; j < k; ++j) {
+    double sp = 0.0, sn = 0.0, mx = -1.0, mv = 0.0, mi = 0.0;
+    for (int64_t r = r0 + t; r < r1; r += 256) {  // rows ascending per thread: first max kept
+      const double u = U[r * k + j];
+      if (u > 0.0) sp = fma(u, u, sp);
+      if (u < 0.0) sn = fma(u, u, sn);
+      if (fabs(u) > mx) {
+        mx = fabs(u);
+        mv = u;
+        mi = (double)r;
+      }
+    }
+    red[t][0] = sp;
+    red[t][1] = sn;
+    red[t][2] = mx;
+    red[t][3] = mv;
+    red[t][4] = mi;
+    __syncthreads();
+    if (t == 0) {  // fixed order; ties on |u|: the lowest row (np.argmax's first occurrence)
+      double a0 = 0.0, a1 = 0.0, bm = -1.0, bv = 0.0, bi = 0.0;
+      for (int i = 0; i < 256; ++i) {
+        a0 += red[i][0];
+        a1 += red[i][1];
+        if (red[i][2] > bm || (red[i][2] == bm && red[i][4] < bi)) {
+          bm = red[i][2];
+          bv = red[i][3];
+          bi = red[i][4];
+        }
+      }
+      double* o = out + ((size_t)blockIdx.x * k + j) * 5;
+      o[0] = a0;
+      o[1] = a1;
+      o[2] = bm;
+      o[3] = bv;
+      o[4] = bi;
+    }
+    __syncthreads();
+  }
+}
+
+// W[n][j] from U[n][j]: v = coef_j · part_j(sign_j · u) with part 0 = |u|, 1 = max(u,0), 2 = |min(u,0)|;
+// v < eps -> 0; then v == 0 -> fill (nndsvda: X.mean(); nndsvd / nndsvdar: 0)
+template <typename TW>
+__global__ __launch_bounds__(256) void ig_fill_kernel(const double* __restrict__ U, int64_t n, int k,
+                                                      const double* __restrict__ coef, const int* __restrict__ part,
+                                                      const double* __restrict__ sgn, double eps, double fill,
+                                                      TW* __restrict__ W) {
+  const int64_t total = n * k;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int j = (int)(e % k);
+    const double u = sgn[j] * U[e];
+    const int pj = part[j];
+    const double p = pj == 0 ? fabs(u) : (pj == 1 ? (u > 0.0 ? u : 0.0) : (u < 0.0 ? -u : 0.0));
+    double v = pj == 0 ? coef[j] * p : p * coef[j];
+    if (v < eps) v = 0.0;
+    if (v == 0.0) v = fill;
+    W[e] = (TW)v;
+  }
 }
 
 }  // namespace cnmf
@@ -4328,7 +4802,101 @@ static int64_t persist_teams_grid(int64_t n_tiles, bool multi, size_t* lds_out) 
   return G;
 }
 
+// ---- variant 4: barrier-free wave tiles (mu_iter_wt_kernel<K, WRES, PD, MULTI>: one 4-wave
+// workgroup per CU, each wave on its own tiles; fp32 X, F = 81, k = 4 (16-sample tiles) or k = 8
+// (8-sample tiles); W resident in LDS when the grid's share fits, else streamed with X).
+// CNMF_WT_PD = prefetch depth 2..4 of the k = 4 W-resident single-GPU kernel (default 3).
+static int wt_pd(int k, bool wres, bool multi) {
+  const char* v = getenv("CNMF_WT_PD");
+  const int pd = v ? atoi(v) : 3;
+  return (k == 4 && wres && !multi && pd >= 2 && pd <= 4) ? pd : 3;
+}
+extern "C++" {
+template <int KK, bool WRES>
+static PassFn wt_fn_k(int pd, bool multi) {
+  if (multi) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true>);
+  if (KK == 4 && WRES && pd == 2) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 2, false>);
+  if (KK == 4 && WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 4, false>);
+  return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false>);
+}
+}
+static PassFn wt_fn(int k, bool wres, bool multi) {
+  const int pd = wt_pd(k, wres, multi);
+  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi) : wt_fn_k<4, false>(pd, multi);
+  return wres ? wt_fn_k<8, true>(pd, multi) : wt_fn_k<8, false>(pd, multi);
+}
+static int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus[dev] = 0;
+  return cus[dev];
+}
+struct WtLaunch {
+  PassFn fn;
+  int64_t G, n_tiles;
+  size_t lds;
+};
+// the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
+// follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
+static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, WtLaunch* out) {
+  if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
+  if (k == 4 && g_persist_variant.load() != 4) return false;
+  const int tsw = 64 / k, wbw = tsw * k * 4;
+  if (n_rows % tsw != 0) return false;
+  const size_t l_wres = k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES;
+  const int ncu = device_cus();
+  const int64_t n_tiles = n_rows / tsw;
+  for (int wres = 1; wres >= 0; --wres) {
+    const int pd = wt_pd(k, wres != 0, multi);
+    // tiles per wave: > PD (the first prefetches), >= 2·PD + 1 when W is streamed (re-load hazard)
+    const int min_nbt = wres ? pd + 1 : 2 * pd + 1;
+    const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
+    if (G < 1) continue;
+    const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
+    const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
+    if (lds > kMaxLds) continue;
+    const PassFn fn = wt_fn(k, wres != 0, multi);
+    if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
+    *out = WtLaunch{fn, G, n_tiles, lds};
+    return true;
+  }
+  return false;
+}
+static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
+                     double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
+                     double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl) {
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+  PersistArgs pa;
+  pa.X = static_cast<const float*>(X);
+  pa.W = static_cast<float*>(W);
+  pa.H64 = H64;
+  pa.Ht = Ht;
+  pa.HHt = HHt;
+  pa.partials = partials;
+  pa.groups = stage;
+  pa.AB = AB;
+  pa.cnt = counter;
+  pa.n_tiles = L.n_tiles;
+  pa.n_iter = n_iter;
+  pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  pa.n_static = 0;
+  pa.l1W = l1_W;
+  pa.l2W = l2_W;
+  pa.l1H = l1_H;
+  pa.l2H = l2_H;
+  pa.apply_first = apply_first;
+  pa.apply_last = apply_last;
+  pa.xctl = xctl;
+  void* args[] = {&pa};
+  HIP_CHECK(hipLaunchKernel(L.fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, s));
+  return CNMF_OK;
+}
+
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
+  WtLaunch L;
+  if (wt_plan(n_rows, x_dtype, n_features, k, false, &L)) return 1;
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
 }
@@ -4341,7 +4909,7 @@ int cnmf_counter_err_word(void) { return CNT_ERR; }
 // system-scope stores and loads over xGMI are coherent with this GPU's while both kernels run.
 constexpr int XBUF_MAX_WORLD = 64;
 static size_t xbuf_bytes(int world) {  // [2 parities][world][2·K·V] tagged 64-bit words
-  return (size_t)2 * world * 2 * sl::K * sl::V * sizeof(uint64_t);
+  return (size_t)2 * world * 2 * wt::Geo<8>::NOUT * sizeof(uint64_t);  // the largest accumulator set
 }
 
 int64_t cnmf_xbuf_bytes(int world) {
@@ -4398,43 +4966,6 @@ int cnmf_xbuf_free(void* dptr) {
   return CNMF_OK;
 }
 
-// ---- variant 4: barrier-free wave tiles (mu_iter_wt_kernel<PD, MULTI>: one 4-wave workgroup per
-// CU, each wave on its own 16-sample tiles, W resident in LDS).  CNMF_WT_PD = prefetch depth (2-4).
-static int wt_pd() {
-  const char* v = getenv("CNMF_WT_PD");
-  const int pd = v ? atoi(v) : 3;
-  return pd >= 2 && pd <= 4 ? pd : 3;
-}
-static PassFn wt_fn(bool multi) {
-  switch (wt_pd()) {
-    case 2: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<2, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<2, false>);
-    case 4: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, false>);
-    default: return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<3, true>) : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<3, false>);
-  }
-}
-// workgroups (0: not eligible) and LDS bytes of a wave-tile launch over n_rows (a persistent shape)
-static int device_cus() {
-  static int cus[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus[dev] = 0;
-  return cus[dev];
-}
-static int64_t wt_grid(int64_t n_rows, bool multi, size_t* lds_out) {
-  if (g_persist_variant.load() != 4 || n_rows % wt::TSW != 0) return 0;
-  const int ncu = device_cus();
-  const int64_t n_tiles = n_rows / wt::TSW;
-  const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * (wt_pd() + 1)), (int64_t)sl::GROUP * sl::MAX_GROUPS});
-  if (G < 1) return 0;
-  const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
-  const size_t lds = (size_t)wt::L_WRES + (size_t)wt::NWV * nbt_max * wt::WBW;
-  if (lds > kMaxLds) return 0;
-  // co-residency of the whole grid (cached per kernel and LDS size; sets the LDS attribute once)
-  if (max_resident(wt_fn(multi), lds) < G) return 0;
-  *lds_out = lds;
-  return G;
-}
-
 // one plain launch of mu_iter_sl_kernel
 static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, double* H64, double* Ht,
                              double* HHt, double* partials, int64_t n_parts, double* stage,
@@ -4466,16 +4997,6 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.xctl = xctl;
   const bool multi = xctl != nullptr;
   void* args[] = {&pa};
-  {
-    size_t wlds_wt = 0;
-    const int64_t GW = wt_grid(n_rows, multi, &wlds_wt);
-    if (GW > 0 && GW <= n_parts) {
-      pa.n_tiles = n_rows / wt::TSW;
-      pa.n_groups = (int)((GW + sl::GROUP - 1) / sl::GROUP);
-      HIP_CHECK(hipLaunchKernel(wt_fn(multi), dim3((unsigned)GW), dim3(NT), args, wlds_wt, s));
-      return CNMF_OK;
-    }
-  }
   if (n_iter > 1) {
     size_t tlds = 0;
     const int64_t GT = persist_teams_grid(n_rows / TS, multi, &tlds);
@@ -4519,6 +5040,13 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     HIP_CHECK(hipMemsetAsync(AB, 0, sizeof(double) * k * (n_features + k), hs));
     return CNMF_OK;
   }
+  {  // one wave-tile launch with n_iter = 1: the multi-iteration launch's layout, so the RCCL path
+     // and the in-launch exchange sum the same partials; only tickets, no waits
+    WtLaunch L;
+    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, &L) && L.G <= n_parts)
+      return launch_wt(L, 1, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
+                       apply_first, 0, hs, nullptr);
+  }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G > 0) {
@@ -4527,14 +5055,6 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     // is the multi-iteration launch's (wave tiles by default), so the RCCL path and the in-launch
     // exchange sum the same fp32 partials.
     if (!partials) return set_err(CNMF_ERR_ARG, "null pointer argument");
-    size_t wlds_wt = 0;
-    const int64_t GW = wt_grid(n_rows, false, &wlds_wt);
-    if (GW > 0 && GW <= n_parts) {
-      if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
-        return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
-      return launch_persistent(G, 1, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB, n_rows,
-                               l1_W, l2_W, l1_H, l2_H, apply_first, 0, hs);
-    }
     if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
       return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
     if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold too few rows");
@@ -4587,6 +5107,19 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                        void* const* events, int n_events, void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   if (n_iter <= 0) return CNMF_OK;
+  {
+    WtLaunch L;
+    if (wt_plan(n_rows, x_dtype, n_features, k, false, &L) && L.G <= n_parts) {
+      if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB)
+        return set_err(CNMF_ERR_ARG, "null pointer argument");
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
+                               l2_H, 0, 1, hs, nullptr);
+      if (st) return st;
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+      return CNMF_OK;
+    }
+  }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G > 0) {
@@ -4645,9 +5178,22 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
                              void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   if (n_iter <= 0) return CNMF_OK;
+  {
+    WtLaunch L;
+    if (wt_plan(n_rows, x_dtype, n_features, k, true, &L) && L.G <= n_parts) {
+      if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
+        return set_err(CNMF_ERR_ARG, "null pointer argument");
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
+                               l2_H, 0, 1, hs, xctl);
+      if (st) return st;
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+      return CNMF_OK;
+    }
+  }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k, true);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
-  if (G == 0) return set_err(CNMF_ERR_UNSUPPORTED, "the in-launch multi-GPU path serves the persistent shape only");
+  if (G == 0) return set_err(CNMF_ERR_UNSUPPORTED, "the in-launch multi-GPU path serves the persistent shapes only");
   if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
@@ -4712,6 +5258,84 @@ int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, 
   const int kF = k * n_features;
   hipLaunchKernelGGL(wmu_basis_kernel, dim3((unsigned)std::min(64, (kF + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), AD, H64, kF);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+// ---- GPU NNDSVD initialisation; see ig_gram_kernel
+static int ig_blocks(int64_t n_rows) {
+  const int ncu = device_cus();
+  const int64_t want = (n_rows + 4095) / 4096;  // >= 4096 rows (64 tiles) per workgroup
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(want, 2 * (int64_t)std::max(ncu, 1)), 1024));
+}
+int64_t cnmf_init_gram_rows(int64_t n_rows) { return n_rows > 0 ? ig_blocks(n_rows) : 0; }
+
+int cnmf_init_gram(const void* X, int x_dtype, int64_t n_rows, int n_features, double* partials,
+                   int64_t n_parts, void* stream) {
+  if (!X || !partials) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_rows < 1 || n_features < 1 || n_features > ig::FP)
+    return set_err(CNMF_ERR_UNSUPPORTED, "GPU init: n_features=%d (1..%d), n_rows=%lld", n_features, ig::FP, (long long)n_rows);
+  const int G = ig_blocks(n_rows);
+  if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the pass needs %d", (long long)n_parts, G);
+  const int64_t rpb = (n_rows + G - 1) / G;
+  const size_t lds = (size_t)ig::GT * ig::FP * 8;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  switch (x_dtype) {
+    case CNMF_F32: hipLaunchKernelGGL(ig_gram_kernel<float>, dim3(G), dim3(256), lds, hs, static_cast<const float*>(X), n_rows, n_features, rpb, partials); break;
+    case CNMF_F64: hipLaunchKernelGGL(ig_gram_kernel<double>, dim3(G), dim3(256), lds, hs, static_cast<const double*>(X), n_rows, n_features, rpb, partials); break;
+    case CNMF_BF16: hipLaunchKernelGGL(ig_gram_kernel<bf16_t>, dim3(G), dim3(256), lds, hs, static_cast<const bf16_t*>(X), n_rows, n_features, rpb, partials); break;
+    default: return set_err(CNMF_ERR_ARG, "x_dtype %d", x_dtype);
+  }
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_init_xm(const void* X, int x_dtype, int64_t n_rows, int n_features, int k, const double* M, double* U,
+                 void* stream) {
+  if (!X || !M || !U) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_rows < 1 || n_features < 1 || n_features > ig::FP || k < 1 || k > ig::KMAX)
+    return set_err(CNMF_ERR_UNSUPPORTED, "GPU init: n_features=%d (1..%d), k=%d (1..%d)", n_features, ig::FP, k, ig::KMAX);
+  const int ncu = device_cus();
+  const int64_t n_tiles = (n_rows + ig::GT - 1) / ig::GT;
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>(n_tiles, 4 * (int64_t)std::max(ncu, 1)));
+  const size_t lds = (size_t)ig::FP * ig::KMAX * 8 + (size_t)ig::GT * (n_features + 1) * 8;
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  switch (x_dtype) {
+    case CNMF_F32: hipLaunchKernelGGL(ig_xm_kernel<float>, dim3(G), dim3(256), lds, hs, static_cast<const float*>(X), n_rows, n_features, k, M, U); break;
+    case CNMF_F64: hipLaunchKernelGGL(ig_xm_kernel<double>, dim3(G), dim3(256), lds, hs, static_cast<const double*>(X), n_rows, n_features, k, M, U); break;
+    case CNMF_BF16: hipLaunchKernelGGL(ig_xm_kernel<bf16_t>, dim3(G), dim3(256), lds, hs, static_cast<const bf16_t*>(X), n_rows, n_features, k, M, U); break;
+    default: return set_err(CNMF_ERR_ARG, "x_dtype %d", x_dtype);
+  }
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int64_t cnmf_init_stats_rows(int64_t n_rows) { return n_rows > 0 ? ig_blocks(n_rows) : 0; }
+
+int cnmf_init_stats(const double* U, int64_t n_rows, int k, double* out, int64_t n_parts, void* stream) {
+  if (!U || !out) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_rows < 1 || k < 1 || k > ig::KMAX) return set_err(CNMF_ERR_SHAPE, "invalid shape");
+  const int G = ig_blocks(n_rows);
+  if (G > n_parts) return set_err(CNMF_ERR_ARG, "out holds %lld rows, the pass needs %d", (long long)n_parts, G);
+  const int64_t rpb = (n_rows + G - 1) / G;
+  hipLaunchKernelGGL(ig_stats_kernel, dim3(G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), U, n_rows, k, rpb, out);
+  HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_init_fill(const double* U, int64_t n_rows, int k, const double* coef, const int* part, const double* sgn,
+                   double eps, double fill, void* W, int w_dtype, void* stream) {
+  if (!U || !coef || !part || !sgn || !W) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (n_rows < 1 || k < 1 || k > ig::KMAX) return set_err(CNMF_ERR_SHAPE, "invalid shape");
+  const int ncu = device_cus();
+  const int G = (int)std::max<int64_t>(1, std::min<int64_t>((n_rows * k + 255) / 256, 8 * (int64_t)std::max(ncu, 1)));
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  if (w_dtype == CNMF_F32)
+    hipLaunchKernelGGL(ig_fill_kernel<float>, dim3(G), dim3(256), 0, hs, U, n_rows, k, coef, part, sgn, eps, fill, static_cast<float*>(W));
+  else if (w_dtype == CNMF_F64)
+    hipLaunchKernelGGL(ig_fill_kernel<double>, dim3(G), dim3(256), 0, hs, U, n_rows, k, coef, part, sgn, eps, fill, static_cast<double*>(W));
+  else
+    return set_err(CNMF_ERR_ARG, "w_dtype %d", w_dtype);
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }

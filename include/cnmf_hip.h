@@ -227,6 +227,32 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
                          int64_t n_parts, int64_t n_rows, int n_features, int k, int flags, void* stream);
 int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, void* stream);
 
+
+/* ---- GPU NNDSVD initialisation (sklearn _initialize_nmf SK:317-373 over
+ * randomized_svd, extmath.py:530-604).  The device does the passes over X; the host the F x r
+ * algebra (cnmf_amd/gpu_init.py).  n_features <= 96, k <= 16.
+ *
+ * cnmf_init_gram: per-workgroup fp64 rows [X^T X (F*F) | column sums of X (F)] into partials
+ *   (cnmf_init_gram_rows(n_rows) rows of F*F + F doubles; reduce them with cnmf_reduce_partials).
+ *   Replaces the X @ Q / X.T @ Q products of _randomized_range_finder (extmath.py:287-357): only
+ *   span(Q) enters the result, and span(X^T X Q) needs only X^T X.
+ * cnmf_init_xm: U = X * M (n_rows x k, fp64), M: F x k fp64 (row-major) — the final U = Q @ Uhat
+ *   (extmath.py:586-590) as one pass over X.
+ * cnmf_init_stats: per workgroup and column j of U: {sum max(u,0)^2, sum min(u,0)^2, max |u|, the u
+ *   at the first row attaining it, that row} (cnmf_init_stats_rows(n_rows) rows of 5k doubles):
+ *   svd_flip's u-based signs (extmath.py:900-953) and the NNDSVD part norms (SK:344-357).
+ * cnmf_init_fill: W[n][j] = coef[j] * part_j(sgn[j] * U[n][j]) (part 0: |u|, 1: max(u,0),
+ *   2: |min(u,0)|), then < eps -> 0, then 0 -> fill (SK:339-369 for nndsvd / nndsvda). */
+int64_t cnmf_init_gram_rows(int64_t n_rows);
+int cnmf_init_gram(const void* X, int x_dtype, int64_t n_rows, int n_features, double* partials,
+                   int64_t n_parts, void* stream);
+int cnmf_init_xm(const void* X, int x_dtype, int64_t n_rows, int n_features, int k, const double* M,
+                 double* U, void* stream);
+int64_t cnmf_init_stats_rows(int64_t n_rows);
+int cnmf_init_stats(const double* U, int64_t n_rows, int k, double* out, int64_t n_parts, void* stream);
+int cnmf_init_fill(const double* U, int64_t n_rows, int k, const double* coef, const int* part,
+                   const double* sgn, double eps, double fill, void* W, int w_dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -94,6 +94,39 @@ def cases():
     return out
 
 
+def init_cases():
+    """(name, X, kwargs) for sklearn's _initialize_nmf (SK:221-373): the NNDSVD family over
+    randomized_svd (extmath.py:530-604), fp64 and fp32, plus init=None's default (nndsvda)."""
+    out = []
+    X64 = iop_spectra(1024, 81, seed=10, dtype=np.float64)
+    for init in ("nndsvd", "nndsvda", "nndsvdar"):
+        out.append((f"init_{init}_float64", X64, dict(n_components=4, init=init, random_state=0)))
+    X32 = iop_spectra(1024, 81, seed=11, dtype=np.float32)
+    for init in ("nndsvda", "nndsvdar"):
+        out.append((f"init_{init}_float32", X32, dict(n_components=4, init=init, random_state=0)))
+    Xr = np.random.RandomState(3).rand(1024, 60)  # well conditioned: every component is signal
+    out.append(("init_rand_k8_float64", Xr, dict(n_components=8, init="nndsvda", random_state=1)))
+    Xd = iop_spectra(1024, 81, seed=12, dtype=np.float32)
+    out.append(("init_default_float32", Xd, dict(n_components=4, init=None, random_state=2)))
+    return out
+
+
+def main_init(manifest):
+    from sklearn.decomposition._nmf import _initialize_nmf
+    manifest["init_generator"] = "sklearn.decomposition._nmf._initialize_nmf"
+    manifest["init_cases"] = {}
+    for name, X, kw in init_cases():
+        W, H = _initialize_nmf(X, kw["n_components"], init=kw["init"], random_state=kw["random_state"])
+        arrays = {"X": X, "W": W, "H": H, "kwargs": np.array(json.dumps(kw))}
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **arrays)
+        with open(path, "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+        manifest["init_cases"][name] = {"sha256": digest, "kwargs": kw, "shape": list(X.shape),
+                                        "dtype": str(X.dtype)}
+        print(f"{name:24s} {str(X.shape):14s} {str(X.dtype):8s} init={kw['init']}")
+
+
 def main():
     from sklearn.decomposition import non_negative_factorization
     import sklearn
@@ -121,6 +154,7 @@ def main():
         manifest["cases"][name] = {"sha256": digest, "kwargs": kw, "n_iter": int(n_iter),
                                    "shape": list(X.shape), "dtype": str(X.dtype)}
         print(f"{name:24s} {str(X.shape):14s} {str(X.dtype):8s} n_iter={n_iter}")
+    main_init(manifest)
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 

@@ -20,6 +20,19 @@ def load(name):
     return case
 
 
+def init_names():
+    with open(os.path.join(GOLDEN, "MANIFEST.json")) as f:
+        return sorted(json.load(f)["init_cases"])
+
+
+def load_init(name):
+    """X, W, H = sklearn's _initialize_nmf(X, **kwargs) (make_golden.py:init_cases)."""
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    case = {k: z[k] for k in z.files}
+    case["kwargs"] = json.loads(str(case["kwargs"]))
+    return case
+
+
 def rel_fro(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

@@ -44,11 +44,13 @@ def _worker(rank, world, port, X, W0, H0, n_iter, tol, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("tol,n_iter", [(0.0, 200), (1e-4, 400)])
-def test_cfg3_sharded_k8_matches_oracle(tol, n_iter):
+@pytest.mark.parametrize("tol,n_iter,N", [(0.0, 200, 40_000 + 37), (1e-4, 400, 40_000 + 37), (0.0, 200, 64 * 700)])
+def test_cfg3_sharded_k8_matches_oracle(tol, n_iter, N):
+    """N = 40037: ragged shards of 20019 / 20018 rows (not whole 8-sample tiles: the per-iteration
+    pass + reduce launches); N = 44800: shards of 22400 rows, each a wave-tile shape (k = 8 wave-tile
+    shard steps + RCCL all-reduce)."""
     import torch.multiprocessing as mp
     from cnmf_amd.synthetic import iop_spectra, random_init
-    N = 40_000 + 37  # ragged: shards of 20019 and 20018 rows, neither a multiple of 64
     X = iop_spectra(N, 81, seed=33, dtype=np.float32)
     W0, H0 = random_init(X, 8, 42)
     ctx = mp.get_context("spawn")
@@ -87,10 +89,13 @@ def test_cfg3_full_shard_k8():
     X = iop_spectra(N, 81, seed=3, dtype=np.float32)
     W0, H0 = random_init(X, 8, 42)
     a, b = _plan(X, W0, H0), _plan(X, W0, H0)
+    assert a.persistent  # the k = 8 wave-tile kernel, W streamed (40 MB of W: no LDS residency)
     a.iterate(20)
-    b.iterate(20)
+    b.iterate(7)
+    b.iterate(13)
     torch.cuda.synchronize()
-    assert torch.equal(a.W, b.W) and torch.equal(a.H64, b.H64)  # bit-for-bit repeatable
+    a.check_sync_error()
+    assert torch.equal(a.W, b.W) and torch.equal(a.H64, b.H64)  # bit-for-bit, across split launches
     Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
                               max_iter=20, tol=0.0)
     W, H = a.W.cpu().numpy(), a.H64.cpu().numpy()
@@ -121,3 +126,26 @@ def test_cfg2_full_size_500_iterations():
     ew, eh = rel_fro(W, Wr), rel_fro(H, Hr)
     print(f"cfg2 500 iterations: rel W {ew:.2e} rel H {eh:.2e}")
     assert ew <= TOL32 and eh <= TOL32, (ew, eh)
+
+
+@pytest.mark.timeout(600)
+def test_wave_tiles_streamed_w_k4():
+    """k = 4 past the LDS-resident W limit (2e6 rows: 31 KB of W per wave would not fit): the
+    wave-tile kernel streams W with X; 30 iterations against the fp64 oracle, repeatable."""
+    import torch
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    N = 2_000_000
+    X = iop_spectra(N, 81, seed=12, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    a, b = _plan(X, W0, H0), _plan(X, W0, H0)
+    assert a.persistent
+    a.iterate(30)
+    b.iterate(12)
+    b.iterate(18)
+    a.check_sync_error()
+    b.check_sync_error()
+    assert torch.equal(a.W, b.W) and torch.equal(a.H64, b.H64)
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=30, tol=0.0)
+    W, H = a.W.cpu().numpy(), a.H64.cpu().numpy()
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))

@@ -30,17 +30,17 @@ def _port():
         return s.getsockname()[1]
 
 
-def _data(N, seed):
+def _data(N, seed, k=4):
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(N, 81, seed=seed, dtype=np.float32)
-    W0, H0 = random_init(X, 4, 42)
+    W0, H0 = random_init(X, k, 42)
     return X, W0, H0
 
 
 def _plan(X, W0, H0, group=None):
     import torch
     from cnmf_amd.solver import MUPlan
-    plan = MUPlan(torch.from_numpy(X).cuda(), 4, group=group)
+    plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1], group=group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
@@ -154,3 +154,31 @@ def test_two_ranks_one_gpu_exchange():
                               max_iter=30, tol=0.0)
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H0_, Hr) <= 1e-5
     assert abs(out[0][2] - out[1][2]) <= 1e-12 * out[0][2]  # the loss all-reduce agrees too
+
+
+@pytest.mark.parametrize("N", [64 * 1500, 1_250_048])
+def test_self_exchange_k8(N):
+    """k = 8 (cfg3's shape) through the in-launch exchange with itself: the wave-tile kernel with W
+    LDS-resident (96k rows) and streamed (a cfg3 shard), bit-identical to the single-GPU launch."""
+    import torch
+    import torch.distributed as dist
+    X, W0, H0 = _data(N, 9, k=8)
+    ref = _plan(X, W0, H0)
+    assert ref.persistent
+    ref.iterate(14)
+    ref.check_sync_error()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        plan = _plan(X, W0, H0, group=dist.group.WORLD)
+        plan.enable_exchange()
+        assert plan.exchange and plan.persistent
+        plan.iterate(5)
+        plan.iterate(9)
+        plan.check_sync_error()
+        torch.cuda.synchronize()
+        assert torch.equal(plan.W, ref.W)
+        assert torch.equal(plan.H64, ref.H64)
+        assert plan.counters_at_rest()
+        plan.release()
+    finally:
+        dist.destroy_process_group()

@@ -68,8 +68,10 @@ def _check_X(X):
         X = X.astype(np.float64)
     if X.shape[0] < 1 or X.shape[1] < 1:
         raise ValueError(f"Found array with shape {X.shape}; a minimum of 1 is required.")
-    if not np.isfinite(X).all():
-        raise ValueError("Input X contains NaN or infinity.")
+    step = max(1, (1 << 26) // X.shape[1])  # row blocks: a memory-mapped X is never held whole
+    for lo in range(0, X.shape[0], step):
+        if not np.isfinite(X[lo:lo + step]).all():
+            raise ValueError("Input X contains NaN or infinity.")
     return np.ascontiguousarray(X)
 
 
@@ -186,10 +188,28 @@ def _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise):
 
 
 _TORCH_DT = {}  # numpy scalar type -> torch dtype, filled on first use
-GPU_INIT_MIN_ROWS = 65536  # below this the host init costs less than a device round trip
+GPU_INIT_MIN_ROWS = 65536
 
 
-def _initial_factors(X, k, init, random_state, device, as_torch, group):
+def _streamed(X, as_torch, memory_budget, solver, Mw):
+    """Out-of-core when a host X is larger than `memory_budget` bytes."""
+    if memory_budget is None:
+        return False
+    if not isinstance(memory_budget, numbers.Integral) or memory_budget <= 0:
+        raise ValueError(f"memory_budget must be a positive number of bytes, got {memory_budget!r}")
+    if as_torch and X.device.type != "cpu":
+        return False  # already in HBM
+    nbytes = X.numel() * X.element_size() if as_torch else X.nbytes
+    if nbytes <= memory_budget:
+        return False
+    if solver != "mu" or Mw is not None:
+        raise ValueError("memory_budget (out-of-core streaming) serves the unweighted 'mu' solver")
+    if as_torch and X.dtype not in (_torch().float32, _torch().float64):
+        raise TypeError("out-of-core streaming takes float32 / float64 X")
+    return True  # below this the host init costs less than a device round trip
+
+
+def _initial_factors(X, k, init, random_state, device, as_torch, group, host_only=False):
     """_initialize_nmf (SK:221-373).  The NNDSVD family on a tall X of one process runs its
     passes over X on the GPU (cnmf_amd.gpu_init, §8 f4); small X, 'random', k > 16 or F > 96, and
     sharded fits (whose X is one shard of the global matrix) take the host restatement."""
@@ -201,7 +221,7 @@ def _initial_factors(X, k, init, random_state, device, as_torch, group):
     resolved = init
     if init is None:
         resolved = "nndsvda" if k <= min(n_samples, n_features) else "random"
-    if (group is None and n_samples >= GPU_INIT_MIN_ROWS and X.min() >= 0
+    if (group is None and not host_only and n_samples >= GPU_INIT_MIN_ROWS and X.min() >= 0
             and _gpu_init.gpu_init_eligible(n_samples, n_features, k, resolved,
                                             X.dtype if as_torch else _TORCH_DT.get(X.dtype.type))):
         dev = torch.device(device) if device is not None else (
@@ -214,7 +234,8 @@ def _initial_factors(X, k, init, random_state, device, as_torch, group):
 
 def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                    l1_ratio, random_state, verbose, device, group=None, return_plan=False,
-                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None):
+                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None,
+                   memory_budget=None):
     """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
     torch = _torch()
     from .solver import ALSPlan, MUPlan, WeightedMUPlan, run_mu
@@ -222,6 +243,7 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
     X = _check_X(X)
     Mw = _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise)
     as_torch = _is_torch(X)
+    streamed = _streamed(X, as_torch, memory_budget, solver, Mw)
     n_samples, n_features = X.shape
     k = n_components
     if k is None:
@@ -257,7 +279,7 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
                           "use them as initialization.", RuntimeWarning)
         if k == "auto":
             k = n_features
-        W, H = _initial_factors(X, int(k), init, random_state, device, as_torch, group)
+        W, H = _initial_factors(X, int(k), init, random_state, device, as_torch, group, host_only=streamed)
     k = int(k)
     if k > 16:
         raise ValueError(f"n_components={k} is not supported: the MI355X kernels handle 1..16.")
@@ -265,18 +287,24 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
         raise ValueError(f"n_components={k} is not supported by solver='als' (1..4).")
 
     regs = _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio)
-    dev = torch.device(device) if device is not None else (X.device if as_torch else torch.device("cuda", torch.cuda.current_device()))
-    Xd = X if as_torch else torch.from_numpy(X)
-    Xd = Xd.to(dev, non_blocking=False).contiguous()
-    if Mw is not None:
-        if k > 8:
-            raise ValueError(f"n_components={k} is not supported by the weighted MU (1..8).")
-        Md = (Mw if _is_torch(Mw) else torch.from_numpy(Mw)).to(dev, torch.float32).contiguous()
-        plan = WeightedMUPlan(Xd, Md, k, group=group)
-    elif solver == "als":
-        plan = ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
+    dev = torch.device(device) if device is not None else (
+        X.device if as_torch and X.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device()))
+    if streamed:  # §8 f3: X stays in host memory and streams through a memory_budget of HBM
+        from .outofcore import StreamedMUPlan
+        plan = StreamedMUPlan(X, k, regs[0], regs[2], regs[1], regs[3], group=group, device=dev,
+                              memory_budget=memory_budget)
     else:
-        plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
+        Xd = X if as_torch else torch.from_numpy(X)
+        Xd = Xd.to(dev, non_blocking=False).contiguous()
+        if Mw is not None:
+            if k > 8:
+                raise ValueError(f"n_components={k} is not supported by the weighted MU (1..8).")
+            Md = (Mw if _is_torch(Mw) else torch.from_numpy(Mw)).to(dev, torch.float32).contiguous()
+            plan = WeightedMUPlan(Xd, Md, k, group=group)
+        elif solver == "als":
+            plan = ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
+        else:
+            plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
     if W is None:  # update_H=False start: sqrt(X.mean()/k) in X's dtype (SK:1228-1232)
         if as_torch:
             avg = float(torch.sqrt(X.double().mean() / k))
@@ -307,7 +335,7 @@ def _out(t, as_torch, X):
 def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
               beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
               l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None,
-              normalise=None, sum_to_one=None, smoothness=0.0, weights=None):
+              normalise=None, sum_to_one=None, smoothness=0.0, weights=None, memory_budget=None):
     """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
@@ -324,6 +352,9 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
     §8(f) row 2, oracle/wmu_ref.py): the loss becomes Σ m·(x − wh)², so a weight 0 marks a missing
     value (give X any finite non-negative entry there) and 1/σ² an uncertainty weight; float32 X,
     k <= 8, no alpha regularisation; tol tests the weighted error.
+    `memory_budget` (bytes; None = off): a host X (NumPy array, memory map or CPU tensor) larger
+    than this is not copied to the GPU whole but streamed through HBM in row chunks every iteration
+    (cnmf_amd.outofcore); same factors as the in-HBM fit up to fp summation order.
     """
     _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
     _validate_normalise(normalise)
@@ -331,7 +362,7 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
     return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                           l1_ratio, random_state, verbose, device, normalise=normalise,
                           solver=solver, sum_to_one=sum_to_one, smoothness=smoothness,
-                          weights=weights)
+                          weights=weights, memory_budget=memory_budget)
 
 
 def _validate_normalise(normalise):
@@ -354,8 +385,9 @@ class NMF:
     def __init__(self, n_components="auto", *, init=None, solver="mu", beta_loss="frobenius",
                  tol=1e-4, max_iter=200, random_state=None, alpha_W=0.0, alpha_H="same",
                  l1_ratio=0.0, verbose=0, shuffle=False, device=None, normalise=None,
-                 sum_to_one=None, smoothness=0.0):
+                 sum_to_one=None, smoothness=0.0, memory_budget=None):
         self.n_components = n_components
+        self.memory_budget = memory_budget
         self.normalise = normalise
         self.sum_to_one = sum_to_one
         self.smoothness = smoothness
@@ -376,7 +408,7 @@ class NMF:
         return {k: getattr(self, k) for k in ("n_components", "init", "solver", "beta_loss", "tol",
                                               "max_iter", "random_state", "alpha_W", "alpha_H",
                                               "l1_ratio", "verbose", "shuffle", "device",
-                                              "normalise", "sum_to_one", "smoothness")}
+                                              "normalise", "sum_to_one", "smoothness", "memory_budget")}
 
     def set_params(self, **params):
         for k, v in params.items():
@@ -397,7 +429,8 @@ class NMF:
             X, W, H, self.n_components, self.init, True, self.tol, self.max_iter, self.alpha_W,
             self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
             return_plan=True, normalise=self.normalise, solver=self.solver,
-            sum_to_one=self.sum_to_one, smoothness=self.smoothness, weights=weights)
+            sum_to_one=self.sum_to_one, smoothness=self.smoothness, weights=weights,
+            memory_budget=self.memory_budget)
         self.reconstruction_err_ = plan.frobenius_error()
         self.n_components_ = int(Hd.shape[0])
         self.components_ = _out(Hd, as_torch, Xc)
@@ -423,7 +456,7 @@ class NMF:
                                  self.tol, self.max_iter, self.alpha_W, self.alpha_H,
                                  self.l1_ratio, self.random_state, self.verbose, self.device,
                                  solver=self.solver, sum_to_one=self.sum_to_one,
-                                 smoothness=self.smoothness)
+                                 smoothness=self.smoothness, memory_budget=self.memory_budget)
         return W
 
     def inverse_transform(self, X=None, *, Xt=None):

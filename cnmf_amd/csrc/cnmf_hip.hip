@@ -2586,6 +2586,7 @@ struct Geo {
   static constexpr int L_WRES = (L_FLAG + 16 + 15) / 16 * 16;           // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
+  static_assert(NOUT * 8 >= NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
 };
 
 template <int CTRL>
@@ -2959,8 +2960,17 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
 
   const int total = a.n_iter * nbt;
   u32x4 pf[PD][PFS];
+  // W streamed: after each of the first PD sets one dummy store (to this workgroup's partial row,
+  // rewritten at the iteration's end), so that every set — the first PD too — has exactly PD stores
+  // younger than it when its step waits (set q < PD: PD - q dummies, then the W stores of bodies
+  // 0..q-1).  Counting PD stores that were never issued would let the set's last loads (the W tile)
+  // still be in flight when it is staged.
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUT) + 64 * w + l;
 #pragma unroll
-  for (int k = 0; k < PD; ++k) prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+  for (int k = 0; k < PD; ++k) {
+    prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+    if (!WRES) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+  }
   // W streamed: a tile's W store (body x) must have retired before its next load is issued (the
   // prefetch at step x + nbt - PD); the step waits retire every operation older than the set they
   // wait for, which covers that store when nbt >= 2·PD + 1 (the host guarantees it)
@@ -2974,7 +2984,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   int cur_i = 0, cur_it = 0, nx_i = PD;
   auto step = [&](u32x4 (&pfk)[PFS]) {
     // younger than this set's loads: the PD-1 later sets and, with W streamed, the W stores of the
-    // PD bodies since (one each)
+    // PD bodies since (one each; for the launch's first PD sets the prologue's dummy stores)
     wait_set<PFS * (PD - 1) + (WRES ? 0 : PD), PFS>(pfk);
     stage(pfk);
     prefetch(pfk, gw + (int64_t)NW * nx_i);
@@ -4946,6 +4956,30 @@ int cnmf_device_can_access_peer(int device, int peer) {
   int ok = 0;
   HIP_CHECK(hipDeviceCanAccessPeer(&ok, device, peer));
   return ok ? 1 : 0;
+}
+
+// ---- host-resident X (out-of-core fits: cnmf_amd/outofcore.py)
+int cnmf_host_register(void* ptr, int64_t bytes) {
+  if (!ptr || bytes <= 0) return set_err(CNMF_ERR_ARG, "null pointer or empty range");
+  const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // a refused registration is reported, not left sticky
+    return set_err(CNMF_ERR_HIP, "hipHostRegister(%lld bytes): %s", (long long)bytes, hipGetErrorString(e));
+  }
+  return CNMF_OK;
+}
+
+int cnmf_host_unregister(void* ptr) {
+  if (!ptr) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  HIP_CHECK(hipHostUnregister(ptr));
+  return CNMF_OK;
+}
+
+int cnmf_copy_h2d_async(void* dst, const void* src, int64_t bytes, void* stream) {
+  if (!dst || !src || bytes < 0) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (bytes == 0) return CNMF_OK;
+  HIP_CHECK(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, reinterpret_cast<hipStream_t>(stream)));
+  return CNMF_OK;
 }
 
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr) {

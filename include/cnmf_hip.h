@@ -253,6 +253,17 @@ int cnmf_init_stats(const double* U, int64_t n_rows, int k, double* out, int64_t
 int cnmf_init_fill(const double* U, int64_t n_rows, int k, const double* coef, const int* part,
                    const double* sgn, double eps, double fill, void* W, int w_dtype, void* stream);
 
+/* ---- Host-resident X (fits whose X exceeds HBM or a memory budget,
+ * cnmf_amd/outofcore.py).  The chunked fit runs cnmf_mu_shard_step per row chunk (apply_first = 0,
+ * AB -> one row per chunk), cnmf_reduce_partials over the chunk rows, then cnmf_basis_update.
+ * cnmf_host_register: page-lock `bytes` of host memory in place (hipHostRegister) so chunk copies
+ *   from it are DMA transfers; fails (status < 0, no sticky error) for memory that cannot be
+ *   locked (e.g. a read-only file mapping): stage through pinned buffers instead.
+ * cnmf_copy_h2d_async: hipMemcpyAsync host -> device on `stream`. */
+int cnmf_host_register(void* ptr, int64_t bytes);
+int cnmf_host_unregister(void* ptr);
+int cnmf_copy_h2d_async(void* dst, const void* src, int64_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

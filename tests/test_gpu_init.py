@@ -35,17 +35,22 @@ def test_gpu_init_matches_sklearn(name):
 
 def test_gpu_init_large_matches_host():
     """cfg2's shape (1e6 x 81 fp32, k = 4): the GPU init against the host restatement (itself
-    pinned to sklearn above) on the same X."""
+    pinned to sklearn above) run in fp64 on the same values.  sklearn's own fp32 path is NOT the
+    yardstick at this size: its fp32 randomized SVD is 1.4e-3 (relative Frobenius, W; 2.5e-3 on the
+    4th component) from the fp64 answer, while the GPU's fp64 Gram form is within 1e-8 of it
+    (measured on CPU with the same algorithm in NumPy)."""
     import torch
     from cnmf_amd.gpu_init import initialize_nmf_gpu
     from cnmf_amd.init import initialize_nmf
     from cnmf_amd.synthetic import iop_spectra
     X = iop_spectra(1_000_000, 81, seed=4, dtype=np.float32)
     Wg, Hg = initialize_nmf_gpu(torch.from_numpy(X).cuda(), 4, init="nndsvda", random_state=0)
-    Wh, Hh = initialize_nmf(X, 4, init="nndsvda", random_state=0)
+    Wh, Hh = initialize_nmf(X.astype(np.float64), 4, init="nndsvda", random_state=0)
     ew, eh = rel_fro(Wg.cpu().numpy(), Wh), rel_fro(Hg, Hh)
-    print(f"1e6 x 81: rel W {ew:.2e} rel H {eh:.2e}")
-    assert ew <= 1e-4 and eh <= 1e-4, (ew, eh)
+    W32, _ = initialize_nmf(X, 4, init="nndsvda", random_state=0)
+    print(f"1e6 x 81: GPU vs fp64 host rel W {ew:.2e} rel H {eh:.2e}; sklearn-fp32 vs fp64 host "
+          f"rel W {rel_fro(W32, Wh):.2e}")
+    assert ew <= 1e-5 and eh <= 1e-5, (ew, eh)
 
 
 def test_api_routes_tall_x_to_gpu_init():
@@ -58,8 +63,8 @@ def test_api_routes_tall_x_to_gpu_init():
     X = iop_spectra(api.GPU_INIT_MIN_ROWS + 1000, 81, seed=6, dtype=np.float32)
     W, H = api._initial_factors(X, 4, None, 3, None, False, None)
     assert isinstance(W, torch.Tensor) and W.is_cuda
-    Wh, Hh = initialize_nmf(X, 4, init=None, random_state=3)
-    assert rel_fro(W.cpu().numpy(), Wh) <= 2e-5 and rel_fro(H, Hh) <= 2e-5
+    Wh, Hh = initialize_nmf(X.astype(np.float64), 4, init=None, random_state=3)  # see above: fp64
+    assert rel_fro(W.cpu().numpy(), Wh) <= 1e-5 and rel_fro(H, Hh) <= 1e-5
     import cnmf_amd
     W1, H1, n = cnmf_amd.factorise(X, n_components=4, random_state=3, max_iter=20, tol=0.0)
     assert n == 20 and W1.shape == (X.shape[0], 4) and np.all(W1 >= 0)

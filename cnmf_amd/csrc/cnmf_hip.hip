@@ -2571,7 +2571,11 @@ struct Geo {
   static constexpr int NCHW = XBW / 16;                     // 324 / 162 chunks
   static constexpr int PFW = (NCHW + 63) / 64;              // 6 / 3 loads per lane
   static constexpr int LASTL = NCHW - 64 * (PFW - 1);       // lanes of the last load: 4 / 34
-  static constexpr int XSTR = XBW + 16;                     // staging stride (16 zero bytes past)
+  // phase 1 reads NQ features from lane e's first one, so the last sample's last lane runs OVR
+  // floats past the tile (features >= F, zero Hᵀ): they must be finite — zeros kept in the slot
+  static constexpr int OVR = (TSW - 1) * F + NQ * NL - XBW / 4;  // 3 (k = 4), 7 (k = 8)
+  static constexpr int PADB = (OVR * 4 + 15) / 16 * 16;          // 16 / 32 zero bytes
+  static constexpr int XSTR = XBW + PADB;                        // staging stride
   static constexpr int WBW = TSW * KK * 4;                  // 256 B of W per tile
   static constexpr int NACC = NQ * KK + KK;                 // fp32 accumulators per lane
   // LDS carve (bytes)
@@ -2585,6 +2589,7 @@ struct Geo {
   static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 4 ints
   static constexpr int L_WRES = (L_FLAG + 16 + 15) / 16 * 16;           // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
+  static_assert(OVR >= 0 && PADB / 4 <= 64, "one zero float per lane covers the overrun");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
   static_assert(NOUT * 8 >= NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
 };
@@ -2894,7 +2899,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   for (int i = t; i < KK * F; i += NT) sH[i] = a.H64[i];
   if (a.apply_first)
     for (int i = t; i < NOUT; i += NT) sAB[i] = a.AB[i];
-  if (l < 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
+  if (l < G_::PADB / 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
   if (WRES)
     for (int c = l; c < nbt * (WBW / 16); c += 64) {
       const int i = c / (WBW / 16), ch = c - i * (WBW / 16);

@@ -69,7 +69,7 @@ def test_streamed_agrees_with_in_hbm_plan_k8():
     m.check_sync_error()
     assert rel_fro(s.W.cpu().numpy(), m.W.cpu().numpy()) < 1e-6
     assert rel_fro(s.H64.cpu().numpy(), m.H64.cpu().numpy()) < 1e-6
-    assert abs(s.frobenius_error() - m.frobenius_error()) <= 1e-9 * m.frobenius_error()
+    assert abs(s.frobenius_error() - m.frobenius_error()) <= 1e-7 * m.frobenius_error()
 
 
 def test_api_memory_budget_tol_matches_oracle():

@@ -307,12 +307,9 @@ def main():
     if args.solver == "mu" and plan.persistent and not args.no_tune:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
-    layout = {4: "wave tiles: one 4-wave workgroup per CU, each wave on its own 16-sample tiles, "
-                 "no barrier inside an iteration, W resident in LDS",
-              1: "pairs of 4-wave workgroups per CU", 2: "one 8-wave two-team workgroup per CU",
-              3: "pairs of 4-wave workgroups per CU with floating tiles (80 % resident, 20 % drawn "
-                 "from a pool every iteration)"}.get(
-        int(plan.lib.cnmf_get_persist_variant())) if plan.persistent else None
+    layout = plan.describe() if plan.persistent else None
+    if layout and "floating" in layout:
+        layout += " (80 % resident, 20 % drawn from a pool every iteration)"
 
     K = args.steps
 

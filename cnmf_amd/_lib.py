@@ -89,6 +89,7 @@ _SIGS = {
     "cnmf_init_stats_rows": (_i64, [_i64]),
     "cnmf_init_stats": (_i32, [_vp, _i64, _i32, _vp, _i64, _vp]),
     "cnmf_init_fill": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _f64, _f64, _vp, _i32, _vp]),
+    "cnmf_persist_describe": (_i32, [_i64, _i32, _i32, _i32, ctypes.c_char_p, _i32]),
     "cnmf_host_register": (_i32, [_vp, _i64]),
     "cnmf_host_unregister": (_i32, [_vp]),
     "cnmf_copy_h2d_async": (_i32, [_vp, _vp, _i64, _vp]),

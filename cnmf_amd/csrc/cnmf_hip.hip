@@ -4916,6 +4916,31 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
 }
 
+int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, char* out, int len) {
+  if (!out || len < 1) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  WtLaunch L;
+  if (wt_plan(n_rows, x_dtype, n_features, k, false, &L)) {
+    const bool wres = L.lds > (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES);
+    snprintf(out, (size_t)len,
+             "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
+             "(%lld workgroups), no barrier inside an iteration",
+             k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
+    return 1;
+  }
+  const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
+  if (g < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+  if (g == 0) {
+    snprintf(out, (size_t)len, "none (per-iteration launches)");
+    return 0;
+  }
+  static const char* names[] = {"", "pairs of 4-wave workgroups per CU", "one 8-wave two-team workgroup per CU",
+                                "pairs of 4-wave workgroups per CU with floating tiles"};
+  const int v = g_persist_variant.load();
+  snprintf(out, (size_t)len, "mu_iter_sl_kernel: %s (%lld workgroups)", (v >= 1 && v <= 3) ? names[v] : "?",
+           (long long)g);
+  return 1;
+}
+
 int64_t cnmf_counter_words(void) { return CNT_WORDS; }
 int cnmf_counter_err_word(void) { return CNT_ERR; }
 

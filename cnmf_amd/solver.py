@@ -263,6 +263,14 @@ class MUPlan:
             raise _lib.HipLibraryError("persistent MU launch timed out waiting for a workgroup "
                                        "(grid not co-resident?); results of that launch are invalid")
 
+    def describe(self) -> str:
+        """The persistent launch this plan's shape takes (kernel, layout, W residency, grid)."""
+        buf = ctypes.create_string_buffer(256)
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_persist_describe(self.n_rows, self.F, self.k, self.xdt, buf, 256),
+                  "cnmf_persist_describe")
+        return buf.value.decode()
+
     def counters_at_rest(self) -> bool:
         """Every ticket, flag, pool and the error word back at zero."""
         return int(self.counter.cpu().numpy().astype("int64").sum()) == 0
@@ -323,8 +331,8 @@ class MUPlan:
         Call after the GPU has been busy for a while (the clock ramps up over the first ~35 ms of
         work).  Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent
         plans."""
-        if not self.persistent:
-            return {}
+        if not self.persistent or self.k != 4 or self.xdt != _lib.F32:
+            return {}  # the layouts are alternatives for fp32 k = 4 only (k = 8: wave tiles)
         W0, H0 = self.W.clone(), self.H64.clone()
         stream = torch.cuda.current_stream(self.device)
         times = {v: [] for v in variants}

@@ -159,6 +159,9 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
  * is bounded: a rank that times out sets the counter's error word and poisons its flags so that
  * every peer's launch fails too; the buffer set is then unusable (fall back to
  * cnmf_mu_shard_step + an RCCL all-reduce). */
+/* The persistent launch cnmf_mu_iterations would use for this shape, as text (kernel, layout,
+ * W residency, grid) into out[len]; returns 1 (persistent), 0 (per-iteration launches) or < 0. */
+int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, char* out, int len);
 int64_t cnmf_xbuf_bytes(int world);
 int cnmf_xbuf_handle_bytes(void);
 /* Peer checks before the exchange: the PCI bus id of a visible device ("dddd:bb:dd.f", len >= 16)

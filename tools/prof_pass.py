@@ -15,13 +15,17 @@ def main():
     ap.add_argument("--features", type=int, default=81)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     a = ap.parse_args()
     import torch
     from cnmf_amd.solver import MUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(a.rows, a.features, seed=0, dtype=np.float32)
     W0, H0 = random_init(X, a.k, 42)
-    plan = MUPlan(torch.from_numpy(X).cuda(), a.k)
+    Xd = torch.from_numpy(X).cuda()
+    if a.dtype == "bf16":
+        Xd = Xd.to(torch.bfloat16)
+    plan = MUPlan(Xd, a.k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     plan.iterate(a.iters)

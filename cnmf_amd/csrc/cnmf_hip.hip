@@ -2605,16 +2605,6 @@ template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
-// lane ^ 4 inside each 8-lane group: row_shr:4 into DPP banks 1 and 3, row_shl:4 into banks 0 and 2
-__device__ __forceinline__ int xor4i(int v) {
-  int r = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xA, false);
-  return __builtin_amdgcn_update_dpp(r, v, 0x104, 0xF, 0x5, false);
-}
-__device__ __forceinline__ double xor4d(double v) {
-  const long long u = __double_as_longlong(v);
-  const int lo = xor4i((int)(u & 0xFFFFFFFFll)), hi = xor4i((int)(u >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
 // v summed over the lanes l' ≡ l (mod NL) of the wave (every lane gets its class's sum)
 template <int NL>
 __device__ __forceinline__ float sum_over_samples(float v) {
@@ -2811,16 +2801,18 @@ __device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
     const int j = e - f * KK;
     sHt[e] = f < wt::F ? (float)sH[j * wt::F + f] : 0.f;
   }
-  const int lane = t & 63;
-  const int wave = t >> 6;
-  for (int e = wave; e < KK * KK; e += NWAVE) {
-    const int j = e / KK;
-    const int m = e - j * KK;
-    double v = 0.0;
-    for (int f = lane; f < wt::F; f += 64) v = fma(sH[j * wt::F + f], sH[m * wt::F + f], v);
-    v = wave_sum(v);
-    if (lane == 0) sHHt[e] = v;
-  }
+  // HHᵀ: NT / K² consecutive threads per entry (16 at k = 4, 4 at k = 8), each a strided part of the
+  // F products, then a fixed xor tree over the group (every entry in the same order; HHᵀ[j][m] and
+  // HHᵀ[m][j] are the same products, so it stays exactly symmetric)
+  constexpr int NE = KK * KK, TPE = NT / NE;
+  static_assert(TPE * NE == NT && (TPE & (TPE - 1)) == 0, "threads per HHᵀ entry: a power of two");
+  const int en = t / TPE, part = t - en * TPE;
+  const int j = en / KK, m = en - (en / KK) * KK;
+  double v = 0.0;
+  for (int f = part; f < wt::F; f += TPE) v = fma(sH[j * wt::F + f], sH[m * wt::F + f], v);
+#pragma unroll
+  for (int o = TPE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (part == 0) sHHt[en] = v;
   __syncthreads();
 }
 // H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728) —
@@ -2915,6 +2907,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // the lane's Hᵀ (fp32 component pairs of each of its NQ features) and HHᵀ row e
   f2 hp[NQ][KP];
   double hh[KK];
+  f2 hh32[KP];  // k = 8: the HHᵀ row in fp32 pairs for the denominator
   auto load_basis = [&]() {
     const float* sHt = reinterpret_cast<const float*>(smem + G_::L_HT);
     const double* sHHt = reinterpret_cast<const double*>(smem + G_::L_HHT);
@@ -2928,6 +2921,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
 #pragma unroll
     for (int m = 0; m < KK; ++m) hh[m] = sHHt[e * KK + m];
+#pragma unroll
+    for (int q = 0; q < KP; ++q) hh32[q] = f2{(float)hh[2 * q], (float)hh[2 * q + 1]};
   };
   load_basis();
 
@@ -3008,53 +3003,64 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     float xv[NQ];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) xv[c] = xr[c];
-    double p[KK];
-#pragma unroll
-    for (int c0 = 0; c0 < NQ; c0 += 7) {
+    double num;
+    if constexpr (KK == 8) {
+      // k = 8: ONE fp32 chain over the lane's 11 features, then the reduce-scatter over the
+      // sample's 8 lanes in fp32 (3 adds per value; a chain of 11 + 3 roundings, below the 7-term
+      // chains' error budget of §4), one DPP move per 32-bit value: level 1 pairs lane e with 7 - e
+      // (row_half_mirror: the other half of components), then e ^ 2 and e ^ 1 (quad_perm)
       f2 ch[KP];
 #pragma unroll
       for (int q = 0; q < KP; ++q) ch[q] = f2{0.f, 0.f};
 #pragma unroll
-      for (int c = c0; c < (c0 + 7 < NQ ? c0 + 7 : NQ); ++c) {
+      for (int c = 0; c < NQ; ++c) {
         const f2 xx = f2{xv[c], xv[c]};
 #pragma unroll
         for (int q = 0; q < KP; ++q) ch[q] = __builtin_elementwise_fma(xx, hp[c][q], ch[q]);
       }
+      const bool b4 = (e & 4) != 0, b2 = (e & 2) != 0, b1 = (e & 1) != 0;
+      f2 r[2];
 #pragma unroll
-      for (int q = 0; q < KP; ++q) {
-        if (c0 == 0) {
-          p[2 * q] = (double)ch[q].x;
-          p[2 * q + 1] = (double)ch[q].y;
-        } else {
-          p[2 * q] += (double)ch[q].x;
-          p[2 * q + 1] += (double)ch[q].y;
+      for (int m = 0; m < 2; ++m) {
+        const f2 keep = b4 ? ch[2 + m] : ch[m], send = b4 ? ch[m] : ch[2 + m];
+        r[m] = keep + f2{dppf<0x141>(send.x), dppf<0x141>(send.y)};  // row_half_mirror
+      }
+      const f2 keep2 = b2 ? r[1] : r[0], send2 = b2 ? r[0] : r[1];
+      const f2 t2 = keep2 + f2{dppf<0x4E>(send2.x), dppf<0x4E>(send2.y)};  // quad_perm [2,3,0,1]
+      const float keep1 = b1 ? t2.y : t2.x, send1 = b1 ? t2.x : t2.y;
+      num = (double)(keep1 + dppf<0xB1>(send1));  // quad_perm [1,0,3,2]
+    } else {
+      // k = 4: packed fp32 chains of 7 features folded into fp64, fp64 reduce-scatter over the
+      // sample's 4 lanes
+      double p[KK];
+#pragma unroll
+      for (int c0 = 0; c0 < NQ; c0 += 7) {
+        f2 ch[KP];
+#pragma unroll
+        for (int q = 0; q < KP; ++q) ch[q] = f2{0.f, 0.f};
+#pragma unroll
+        for (int c = c0; c < (c0 + 7 < NQ ? c0 + 7 : NQ); ++c) {
+          const f2 xx = f2{xv[c], xv[c]};
+#pragma unroll
+          for (int q = 0; q < KP; ++q) ch[q] = __builtin_elementwise_fma(xx, hp[c][q], ch[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < KP; ++q) {
+          if (c0 == 0) {
+            p[2 * q] = (double)ch[q].x;
+            p[2 * q + 1] = (double)ch[q].y;
+          } else {
+            p[2 * q] += (double)ch[q].x;
+            p[2 * q + 1] += (double)ch[q].y;
+          }
         }
       }
-    }
-    // reduce-scatter over the NL lanes of the sample: lane e ends with num[s][e] (fp64)
-    double num;
-    {
       const bool b1 = (e & 1) != 0, b2 = (e & 2) != 0;
       double k2[2];
-      if constexpr (KK == 8) {
-        const bool b4 = (e & 4) != 0;
-        double k4[4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const double keep = b4 ? p[4 + m] : p[m], send = b4 ? p[m] : p[4 + m];
-          k4[m] = keep + xor4d(send);
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const double keep = b2 ? k4[2 + m] : k4[m], send = b2 ? k4[m] : k4[2 + m];
-          k2[m] = keep + dpp64<0x4E>(send);  // quad_perm [2,3,0,1]
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const double keep = b2 ? p[2 + m] : p[m], send = b2 ? p[m] : p[2 + m];
-          k2[m] = keep + dpp64<0x4E>(send);
-        }
+      for (int m = 0; m < 2; ++m) {
+        const double keep = b2 ? p[2 + m] : p[m], send = b2 ? p[m] : p[2 + m];
+        k2[m] = keep + dpp64<0x4E>(send);  // quad_perm [2,3,0,1]
       }
       const double keep = b1 ? k2[1] : k2[0], send = b1 ? k2[0] : k2[1];
       num = keep + dpp64<0xB1>(send);  // quad_perm [1,0,3,2]
@@ -3072,8 +3078,17 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     const double wold = (double)wt_[s * KK + e];
     double den = 0.0;
+    if constexpr (KK == 8) {
+      // den = w·HHᵀ[e] in packed fp32 (8 positive terms: no cancellation, ≤ 8 roundings), the
+      // update itself in fp64
+      f2 d2 = f2{0.f, 0.f};
 #pragma unroll
-    for (int m = 0; m < KK; ++m) den = fma((double)wv[m], hh[m], den);
+      for (int q = 0; q < KP; ++q) d2 = __builtin_elementwise_fma(f2{wv[2 * q], wv[2 * q + 1]}, hh32[q], d2);
+      den = (double)(d2.x + d2.y);
+    } else {
+#pragma unroll
+      for (int m = 0; m < KK; ++m) den = fma((double)wv[m], hh[m], den);
+    }
     if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
     if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
     if (den == 0.0) den = EPS32;                // SK:620

@@ -23,6 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1000, help="iterations before the stamped launch (clock ramp)")
     ap.add_argument("--exchange", action="store_true",
                     help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
@@ -32,7 +33,7 @@ def main():
     from cnmf_amd.solver import MUPlan
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(a.rows, 81, seed=0, dtype=np.float32)
-    W0, H0 = random_init(X, 4, 42)
+    W0, H0 = random_init(X, a.k, 42)
     lib = _lib.load()
     fn = lib.cnmf_debug_timeline
     fn.argtypes = [ctypes.c_void_p]
@@ -46,7 +47,7 @@ def main():
             port = so.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         group = dist.group.WORLD
-    plan = MUPlan(torch.from_numpy(X).cuda(), 4, group=group)
+    plan = MUPlan(torch.from_numpy(X).cuda(), a.k, group=group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     if a.exchange:

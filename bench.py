@@ -304,7 +304,7 @@ def main():
     # the persistent launch has several layouts whose order can differ between boxes: time them on
     # this box (warm clocks; copies of W / H, so the state is unchanged) and keep the fastest
     tuned = {}
-    if args.solver == "mu" and plan.persistent and not args.no_tune:
+    if args.solver == "mu" and plan.persistent and not args.no_tune and not args.weighted:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
     layout = plan.describe() if plan.persistent else None
@@ -383,7 +383,10 @@ def main():
     traffic, traffic_src = (None, None) if (args.solver == "als" or args.weighted) else load_traffic(args.traffic_json, n_rows, F, k)
     if traffic is not None:
         traffic = traffic * iters_per_launch
-    if args.weighted:
+    if args.weighted and persistent:
+        kname = ("wmu_iter_wt_kernel (persistent: K weighted iterations of pass + in-launch reduction + "
+                 "H-step per launch)")
+    elif args.weighted:
         kname = "weighted MU pass (wmu_pass_kernel: W-step + [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))])"
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"

@@ -4349,6 +4349,412 @@ __global__ __launch_bounds__(256) void wmu_basis_kernel(const double* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// wmu_iter_wt_kernel — n weighted MU iterations as ONE persistent launch (fp32 X and M, F = 81,
+// k = 4, W resident in LDS).  The layout is mu_iter_wt_kernel's (§3.0 of DESIGN.md): one 4-wave
+// workgroup per CU, each wave on its own 16-sample tiles (the same tiles every iteration), no
+// barrier inside an iteration, the next tiles' X AND M prefetched into AGPRs by counted loads, the
+// workgroup's fp64 row reduced in-launch by the ticket tree, every workgroup applying the H-step
+// itself.  Lane l = 4s + e of a tile: sample s, features [21e, 21e + 21) (the lanes past F read
+// zero-Hᵀ pads).  Per tile (the arithmetic of wmu_pass_kernel, oracle/wmu_ref.py):
+//   phase 1  rec_f = w·h_f, mx_f = m_f·x_f, mr_f = m_f·rec_f; num_j = Σ_f mx_f·h_jf and
+//            den_j = Σ_f mr_f·h_jf over the lane's features in packed fp32 chains of 7 folded into
+//            fp64, then the fp64 reduce-scatter over the sample's 4 lanes: lane e owns (num_e,
+//            den_e); w'_e = w_e·num_e/den_e (den = 0 -> EPS32)
+//   phase 3  rec'_f = w'·h_f; A_jf += w'_j·mx_f, D_jf += w'_j·m_f·rec'_f (fp32 per lane over the
+//            iteration's tiles)
+// End of an iteration: each lane class's sums over the wave's 16 sample lanes, the 4 waves in wave
+// order in fp64 -> the workgroup's row [A | D] (2kF = 648 doubles), the ticket tree -> AD, and
+// H <- H∘A/D (D = 0 -> EPS32) in every workgroup.  Deterministic: no order depends on arrival.
+// ------------------------------------------------------------------------------------------------
+namespace ww {
+using G4 = wt::Geo<4>;
+constexpr int K = 4, NL = 4, TSW = 16, F = wt::F, NQ = G4::NQ, KF = K * F;
+constexpr int NOUT = 2 * KF;             // [A | D]
+constexpr int NACC = 2 * NQ * K;         // fp32 accumulators per lane: A then D
+constexpr int L_STG = 0;                 // [NWV][2][XSTR]: the wave's X slot, then its M slot
+constexpr int L_RED = L_STG + wt::NWV * 2 * G4::XSTR;          // [NWV][NL][NACC] fp32
+constexpr int L_H = L_RED + wt::NWV * NL * NACC * 4;           // H fp64 [K][F]
+constexpr int L_AB = L_H + KF * 8;                             // AD fp64 [NOUT]
+constexpr int L_HT = L_AB + NOUT * 8;                          // Hᵀ fp32 [NL·NQ][K]
+constexpr int L_FLAG = L_HT + NL * NQ * K * 4;                 // 4 ints
+constexpr int L_WRES = (L_FLAG + 16 + 15) / 16 * 16;           // [NWV][nbt_max][WBW]
+static_assert(L_RED % 16 == 0 && L_HT % 16 == 0, "16-byte aligned LDS regions");
+static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
+}  // namespace ww
+
+struct WmuPersistArgs {
+  const float* X;
+  const float* M;
+  float* W;
+  double* H64;       // in: the basis; out: the final basis
+  double* partials;  // [G][NOUT] per-workgroup rows
+  double* groups;    // [NG][NOUT] group rows
+  double* AD;        // [NOUT]: out (the last iteration's reduced accumulators)
+  uint32_t* cnt;     // CNT_WORDS counters (at rest on entry, left at rest)
+  int64_t n_tiles;
+  int n_iter;
+  int n_groups;
+};
+
+// Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) from the fp64 H in LDS
+__device__ __forceinline__ void ww_derive_basis(unsigned char* smem, int t) {
+  const double* sH = reinterpret_cast<const double*>(smem + ww::L_H);
+  float* sHt = reinterpret_cast<float*>(smem + ww::L_HT);
+  for (int e = t; e < ww::NL * ww::NQ * ww::K; e += NT) {
+    const int f = e / ww::K;
+    const int j = e - f * ww::K;
+    sHt[e] = f < ww::F ? (float)sH[j * ww::F + f] : 0.f;
+  }
+  __syncthreads();
+}
+// H <- H ∘ A / D from AD in LDS (D = 0 -> EPS32; oracle/wmu_ref.update_h), then Hᵀ
+__device__ __forceinline__ void ww_update_basis(unsigned char* smem, int t) {
+  constexpr int U = (ww::KF + NT - 1) / NT;
+  double* sH = reinterpret_cast<double*>(smem + ww::L_H);
+  const double* sAD = reinterpret_cast<const double*>(smem + ww::L_AB);
+  double hn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + NT * u;
+    hn[u] = 0.0;
+    if (e < ww::KF) {
+      double d = sAD[ww::KF + e];
+      if (d == 0.0) d = EPS32;
+      hn[u] = sH[e] * (sAD[e] / d);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (t + NT * u < ww::KF) sH[t + NT * u] = hn[u];
+  __syncthreads();
+  ww_derive_basis(smem, t);
+}
+
+namespace cnmf::wt {
+template <int N>
+__device__ __forceinline__ void wait_set12(u32x4 (&pf)[12]) {
+  asm volatile("s_waitcnt vmcnt(%12)"
+               : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5]), "+a"(pf[6]),
+                 "+a"(pf[7]), "+a"(pf[8]), "+a"(pf[9]), "+a"(pf[10]), "+a"(pf[11])
+               : "n"(N) : "memory");
+}
+}  // namespace cnmf::wt
+
+template <int PD>
+__global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
+  using namespace wt;
+  using G4 = Geo<4>;
+  constexpr int KK = ww::K, NL = ww::NL, TSW = ww::TSW, NQ = ww::NQ, NOUT = ww::NOUT, NACC = ww::NACC;
+  constexpr int KF = ww::KF;
+  constexpr int XBW = G4::XBW, XSTR = G4::XSTR, WBW = G4::WBW, PFW = G4::PFW, LASTL = G4::LASTL;
+  constexpr int PFS = 2 * PFW;  // loads per prefetch set: the X tile, then the M tile
+  static_assert(PFS == 12, "wait_set12");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int s = l / NL, e = l % NL;
+  const int b = blockIdx.x;
+  const int G = gridDim.x;
+  const int NW = NWV * G;
+  const int gw = NWV * b + w;
+  const int NG = a.n_groups;
+  const int g = b % NG;
+  const int gs = (G - g + NG - 1) / NG;
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
+  const unsigned char* Mb = reinterpret_cast<const unsigned char*>(a.M);
+  unsigned char* Wb = reinterpret_cast<unsigned char*>(a.W);
+  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);  // this wave's tiles per iteration
+  const int nbt_max = (int)((a.n_tiles + NW - 1) / NW);
+  unsigned char* stx = smem + ww::L_STG + 2 * w * XSTR;
+  unsigned char* stm = stx + XSTR;
+  float* wres = reinterpret_cast<float*>(smem + ww::L_WRES + (size_t)w * nbt_max * WBW);  // [i][TSW][K]
+  float* red = reinterpret_cast<float*>(smem + ww::L_RED);
+  double* sH = reinterpret_cast<double*>(smem + ww::L_H);
+  double* sAD = reinterpret_cast<double*>(smem + ww::L_AB);
+  int* sFlag = reinterpret_cast<int*>(smem + ww::L_FLAG);
+  uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
+  uint32_t* cnt_top = a.cnt + CNT_TOP;
+  uint32_t* flag = a.cnt + CNT_FLAG;
+  uint32_t* err = a.cnt + CNT_ERR;
+
+  // ---- the basis, the staging pads (finite zeros past both slots), this wave's W tiles
+  for (int i = t; i < KF; i += NT) sH[i] = a.H64[i];
+  if (l < G4::PADB / 4) {
+    reinterpret_cast<float*>(stx + XBW)[l] = 0.f;
+    reinterpret_cast<float*>(stm + XBW)[l] = 0.f;
+  }
+  for (int c = l; c < nbt * (WBW / 16); c += 64) {
+    const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
+    *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
+        *reinterpret_cast<const u32x4*>(Wb + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
+  }
+  __syncthreads();
+  ww_derive_basis(smem, t);
+
+  // the lane's Hᵀ: fp32 component pairs of each of its NQ features
+  f2 hp[NQ][2];
+  auto load_basis = [&]() {
+    const float* sHt = reinterpret_cast<const float*>(smem + ww::L_HT);
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const float4 h = *reinterpret_cast<const float4*>(sHt + (NQ * e + c) * KK);
+      hp[c][0] = f2{h.x, h.y};
+      hp[c][1] = f2{h.z, h.w};
+    }
+  };
+  load_basis();
+
+  f2 accA[NQ][2], accD[NQ][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int c = 0; c < NQ; ++c)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        accA[c][q] = f2{0.f, 0.f};
+        accD[c][q] = f2{0.f, 0.f};
+      }
+  };
+  zero_acc();
+
+  // the tile's 16-byte chunks of this lane in X, then the same chunks of M (lanes >= LASTL re-load
+  // chunk l for the last load: never staged; every lane issues the same loads)
+  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile) {
+    const size_t off = (size_t)tile * XBW + 16 * l;
+#pragma unroll
+    for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], Xb + off + 1024 * u);
+    ld16(pf[PFW - 1], Xb + (l < LASTL ? off + 1024 * (PFW - 1) : off));
+#pragma unroll
+    for (int u = 0; u < PFW - 1; ++u) ld16(pf[PFW + u], Mb + off + 1024 * u);
+    ld16(pf[2 * PFW - 1], Mb + (l < LASTL ? off + 1024 * (PFW - 1) : off));
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS]) {
+    const unsigned ax = (unsigned)(uintptr_t)(stx + 16 * l);
+    const unsigned am = (unsigned)(uintptr_t)(stm + 16 * l);
+    stage_rec<0, PFW - 1>(ax, pf);
+    if (l < LASTL) st16<1024 * (PFW - 1)>(ax, pf[PFW - 1]);
+    stage_rec<0, PFW - 1>(am, pf + PFW);
+    if (l < LASTL) st16<1024 * (PFW - 1)>(am, pf[2 * PFW - 1]);
+  };
+
+  const int total = a.n_iter * nbt;
+  u32x4 pf[PD][PFS];
+#pragma unroll
+  for (int k = 0; k < PD; ++k) prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+  TL_START;
+
+  bool alive = true;
+  int cur_i = 0, cur_it = 0, nx_i = PD;
+  auto step = [&](u32x4 (&pfk)[PFS]) {
+    wait_set12<PFS * (PD - 1)>(pfk);  // the PD - 1 younger sets stay in flight
+    stage(pfk);
+    prefetch(pfk, gw + (int64_t)NW * nx_i);
+    if (++nx_i == nbt) nx_i = 0;
+  };
+  auto body = [&]() {
+    const int it = cur_it, i = cur_i;
+    if (++cur_i == nbt) {
+      cur_i = 0;
+      ++cur_it;
+    }
+    const bool last_it = it + 1 == a.n_iter;
+    // phase 1
+    const float* xr = reinterpret_cast<const float*>(stx) + s * wt::F + NQ * e;
+    const float* mr = reinterpret_cast<const float*>(stm) + s * wt::F + NQ * e;
+    float mv[NQ], mx[NQ];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      mv[c] = mr[c];
+      mx[c] = mv[c] * xr[c];
+    }
+    float* wt_ = wres + i * (TSW * KK);
+    const float4 w4 = *reinterpret_cast<const float4*>(wt_ + s * KK);
+    const f2 w01 = f2{w4.x, w4.y}, w23 = f2{w4.z, w4.w};
+    const double wold = (double)(e == 0 ? w4.x : (e == 1 ? w4.y : (e == 2 ? w4.z : w4.w)));
+    double pn[KK], pd[KK];
+#pragma unroll
+    for (int c0 = 0; c0 < NQ; c0 += 7) {
+      f2 cn[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}}, cd[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+      for (int c = c0; c < c0 + 7; ++c) {
+        f2 r2 = w01 * hp[c][0];
+        r2 = __builtin_elementwise_fma(w23, hp[c][1], r2);
+        const float mrc = mv[c] * (r2.x + r2.y);
+        const f2 xx = f2{mx[c], mx[c]}, rr = f2{mrc, mrc};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          cn[q] = __builtin_elementwise_fma(xx, hp[c][q], cn[q]);
+          cd[q] = __builtin_elementwise_fma(rr, hp[c][q], cd[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (c0 == 0) {
+          pn[2 * q] = (double)cn[q].x;
+          pn[2 * q + 1] = (double)cn[q].y;
+          pd[2 * q] = (double)cd[q].x;
+          pd[2 * q + 1] = (double)cd[q].y;
+        } else {
+          pn[2 * q] += (double)cn[q].x;
+          pn[2 * q + 1] += (double)cn[q].y;
+          pd[2 * q] += (double)cd[q].x;
+          pd[2 * q + 1] += (double)cd[q].y;
+        }
+      }
+    }
+    // reduce-scatter over the sample's 4 lanes (fp64): lane e keeps component e
+    const bool b1 = (e & 1) != 0, b2 = (e & 2) != 0;
+    double kn[2], kd[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const double keepn = b2 ? pn[2 + m] : pn[m], sendn = b2 ? pn[m] : pn[2 + m];
+      const double keepd = b2 ? pd[2 + m] : pd[m], sendd = b2 ? pd[m] : pd[2 + m];
+      kn[m] = keepn + dpp64<0x4E>(sendn);  // quad_perm [2,3,0,1]
+      kd[m] = keepd + dpp64<0x4E>(sendd);
+    }
+    const double num = (b1 ? kn[1] : kn[0]) + dpp64<0xB1>(b1 ? kn[0] : kn[1]);  // quad_perm [1,0,3,2]
+    double den = (b1 ? kd[1] : kd[0]) + dpp64<0xB1>(b1 ? kd[0] : kd[1]);
+    if (den == 0.0) den = EPS32;
+    const float wn = (float)(wold * (num / den));
+    wt_[s * KK + e] = wn;
+    // phase 3 with the sample's new row (this wave's writes above precede the read)
+    const float4 p4 = *reinterpret_cast<const float4*>(wt_ + s * KK);
+    const f2 wp[2] = {f2{p4.x, p4.y}, f2{p4.z, p4.w}};
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      f2 r2 = wp[0] * hp[c][0];
+      r2 = __builtin_elementwise_fma(wp[1], hp[c][1], r2);
+      const float mrc = mv[c] * (r2.x + r2.y);
+      const f2 xx = f2{mx[c], mx[c]}, rr = f2{mrc, mrc};
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        accA[c][q] = __builtin_elementwise_fma(xx, wp[q], accA[c][q]);
+        accD[c][q] = __builtin_elementwise_fma(rr, wp[q], accD[c][q]);
+      }
+    }
+    if (i + 1 != nbt) return;
+
+    // ---- end of this wave's iteration: its sums over the sample lanes of each e -> LDS
+    {
+      float* rw = red + (w * NL + e) * NACC;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        const float4 va = make_float4(sum_over_samples<NL>(accA[c][0].x), sum_over_samples<NL>(accA[c][0].y),
+                                      sum_over_samples<NL>(accA[c][1].x), sum_over_samples<NL>(accA[c][1].y));
+        const float4 vd = make_float4(sum_over_samples<NL>(accD[c][0].x), sum_over_samples<NL>(accD[c][0].y),
+                                      sum_over_samples<NL>(accD[c][1].x), sum_over_samples<NL>(accD[c][1].y));
+        if (l < NL) {
+          *reinterpret_cast<float4*>(rw + c * KK) = va;
+          *reinterpret_cast<float4*>(rw + NQ * KK + c * KK) = vd;
+        }
+      }
+    }
+    zero_acc();
+    __syncthreads();
+    // the workgroup's fp64 row [A | D]: the four waves' sums in wave order (deterministic)
+    {
+      double* prow = a.partials + (size_t)b * NOUT;
+      for (int o = t; o < NOUT; o += NT) {
+        const int isd = o >= KF ? 1 : 0;
+        const int r = o - isd * KF;
+        const int j = r / wt::F;
+        const int f = r - j * wt::F;
+        const int ee = f / NQ;
+        const float* rr = red + ee * NACC + isd * NQ * KK + (f - NQ * ee) * KK + j;
+        constexpr int WS = NL * NACC;  // wave stride
+        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
+    __syncthreads();
+    TL(it, 0);
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
+      sFlag[1] = 0;
+      sFlag[2] = 1;
+    }
+    __syncthreads();
+    if (sFlag[0]) {  // group combiner
+      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
+      }
+      __syncthreads();
+      if (sFlag[1]) {  // top combiner: AD
+        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAD, a.AD, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0 && !last_it)
+          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TL_PUB(it);
+      }
+    }
+    const bool top = sFlag[1] != 0;
+    if (last_it) {
+      alive = false;
+      for (int c = l; c < nbt * (WBW / 16); c += 64) {  // this wave's W back to HBM, once per launch
+        const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+        *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+            *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
+      }
+      if (!top) return;
+      // the last combiner of the launch: every other workgroup has arrived for the last time
+      ww_update_basis(smem, t);
+      for (int o = t; o < KF; o += NT) a.H64[o] = sH[o];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
+        alive = false;
+        return;
+      }
+      for (int o = t; o < NOUT; o += NT) sAD[o] = ld_sc1(a.AD + o);
+      __syncthreads();
+    }
+    ww_update_basis(smem, t);
+    load_basis();
+    TL(it, 1);
+  };
+
+  for (int p = 0; p < total && alive; p += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      step(pf[k]);
+      if (p + k < total && alive) body();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+}
+
 // tile size of the weighted pass: the largest of 64 / 32 / 16 / 8 samples whose LDS fits 64 KB
 static int wmu_tile(int F, int KP) {
   for (int ts = 64; ts >= 8; ts >>= 1) {
@@ -4893,6 +5299,27 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, WtLau
   }
   return false;
 }
+// the weighted wave-tile launch for this shape, or false (not served: the per-iteration pass)
+struct WwLaunch {
+  int64_t G, n_tiles;
+  size_t lds;
+};
+static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out) {
+  constexpr int PD = 2;
+  if (F != wt::F || k != ww::K || n_rows <= 0 || n_rows % ww::TSW != 0) return false;
+  if (getenv("CNMF_WMU_PERSIST") && atoi(getenv("CNMF_WMU_PERSIST")) == 0) return false;
+  const int64_t n_tiles = n_rows / ww::TSW;
+  const int64_t G = std::min<int64_t>({(int64_t)device_cus(), n_tiles / (wt::NWV * (PD + 1)),
+                                       (int64_t)sl::GROUP * sl::MAX_GROUPS});
+  if (G < 1) return false;
+  const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
+  const size_t lds = (size_t)ww::L_WRES + (size_t)wt::NWV * nbt_max * wt::Geo<4>::WBW;
+  if (lds > kMaxLds) return false;  // W does not fit in LDS: the per-iteration pass serves it
+  if (max_resident(reinterpret_cast<PassFn>(&wmu_iter_wt_kernel<PD>), lds) < G) return false;
+  *out = WwLaunch{G, n_tiles, lds};
+  return true;
+}
+
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
                      double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
                      double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl) {
@@ -5328,6 +5755,47 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
   hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(NT), lds, hs, X, M, W, H64, partials, n_rows, n_features, k, ts,
                      flags, n_tiles, rows);
   HIP_CHECK(hipGetLastError());
+  return CNMF_OK;
+}
+
+int cnmf_wmu_persistent(int64_t n_rows, int n_features, int k) {
+  WwLaunch L;
+  return ww_plan(n_rows, n_features, k, &L) ? 1 : 0;
+}
+
+int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                        int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                        int n_features, int k, void* const* events, int n_events, void* stream) {
+  if (n_iter <= 0) return CNMF_OK;
+  WwLaunch L;
+  if (!ww_plan(n_rows, n_features, k, &L))
+    return set_err(CNMF_ERR_UNSUPPORTED, "the persistent weighted MU serves fp32 F=81 k=4 with rows a multiple "
+                   "of 16 whose W fits in LDS (n_rows=%lld F=%d k=%d)", (long long)n_rows, n_features, k);
+  if (!X || !M || !W || !H64 || !partials || !stage || !counter || !AD)
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(M) & 15) ||
+      (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X, the weights and W must be 16-byte aligned");
+  if (L.G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
+                                    (long long)n_parts, (long long)L.G);
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  WmuPersistArgs pa;
+  pa.X = X;
+  pa.M = M;
+  pa.W = W;
+  pa.H64 = H64;
+  pa.partials = partials;
+  pa.groups = stage;
+  pa.AD = AD;
+  pa.cnt = counter;
+  pa.n_tiles = L.n_tiles;
+  pa.n_iter = n_iter;
+  pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  void* args[] = {&pa};
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(&wmu_iter_wt_kernel<2>), dim3((unsigned)L.G), dim3(NT),
+                            args, L.lds, hs));
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;
 }
 

@@ -501,7 +501,11 @@ class WeightedMUPlan:
     Per iteration: one pass over X and the weights M (`cnmf_wmu_sample_pass`: the W-step and the
     per-workgroup fp64 rows [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))]), the deterministic fp64 reduction, (multi-GPU:
     one all_reduce of the 2kF accumulators,) and the H-step (`cnmf_wmu_basis_update`).  The same
-    driver (`run_mu`) runs it: W then H, the weighted error every 10 iterations when tol > 0."""
+    driver (`run_mu`) runs it: W then H, the weighted error every 10 iterations when tol > 0.
+
+    Single GPU at the served shape (fp32, F = 81, k = 4, rows a multiple of 16, W fits in LDS;
+    `cnmf_wmu_persistent`): n iterations are ONE launch of the persistent weighted kernel
+    (`cnmf_wmu_iterations`: pass, in-launch reduction and H-step per iteration)."""
 
     persistent = persistent_shape = exchange = False
 
@@ -533,6 +537,11 @@ class WeightedMUPlan:
         self.counter = torch.zeros(int(self.lib.cnmf_counter_words()), dtype=torch.int32, device=dev)
         self.AD = torch.zeros(self.n_out, dtype=f64, device=dev)
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
+        self.err_word = int(self.lib.cnmf_counter_err_word())
+        with torch.cuda.device(self.device):
+            p = self.lib.cnmf_wmu_persistent(self.n_rows, self.F, self.k)
+        self.persistent_shape = bool(check(p, "cnmf_wmu_persistent"))
+        self.persistent = self.persistent_shape and self.world == 1
 
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -567,8 +576,28 @@ class WeightedMUPlan:
         if self.world > 1:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
+    def refresh_basis(self):
+        pass  # the weighted kernels read H64 itself
+
+    def describe(self) -> str:
+        if self.persistent:
+            return ("wmu_iter_wt_kernel<k=4, W resident in LDS, PD=2>: wave tiles of 16 samples, X and the "
+                    "weights prefetched together, one 4-wave workgroup per CU, in-launch reduction and H-step")
+        return "wmu_pass_kernel + cnmf_reduce_partials + wmu_basis_kernel per iteration"
+
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
-        """n_iter weighted MU iterations; pass_events: 2·n_iter events recorded around each pass."""
+        """n_iter weighted MU iterations; pass_events: 2 events around the one launch when
+        self.persistent, else 2·n_iter events recorded around each pass."""
+        if n_iter <= 0:
+            return
+        if self.persistent and update_H:
+            with torch.cuda.device(self.device):
+                check(self.lib.cnmf_wmu_iterations(
+                    n_iter, _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64),
+                    _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
+                    _ptr(self.AD), self.n_rows, self.F, self.k, *_event_array(pass_events),
+                    self._stream()), "cnmf_wmu_iterations")
+            return
         ev = list(pass_events) if pass_events is not None else None
         stream = torch.cuda.current_stream(self.device) if ev is not None else None
         for i in range(max(n_iter, 0)):
@@ -590,7 +619,11 @@ class WeightedMUPlan:
                                                  self._stream()), "cnmf_wmu_basis_update")
 
     def check_sync_error(self):
-        pass  # no in-launch waits in the weighted path
+        """Raise if the persistent launch gave up waiting for a workgroup (results invalid)."""
+        if self.persistent_shape and int(self.counter[self.err_word].item()) != 0:
+            self.counter.zero_()
+            raise _lib.HipLibraryError("persistent weighted MU launch timed out waiting for a workgroup "
+                                       "(grid not co-resident?); results of that launch are invalid")
 
     def frobenius_error(self) -> float:
         """sqrt(Σ m·(x − w·h)²) over all ranks; synchronises."""

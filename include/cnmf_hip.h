@@ -230,6 +230,22 @@ int cnmf_wmu_sample_pass(const float* X, const float* M, float* W, const double*
                          int64_t n_parts, int64_t n_rows, int n_features, int k, int flags, void* stream);
 int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, void* stream);
 
+/* n weighted MU iterations (W-step, [A | D] of the new W, H-step) as ONE persistent launch
+ * (wmu_iter_wt_kernel: the in-launch reduction and H-step of cnmf_mu_iterations' wave-tile kernel).
+ * Served shape (cnmf_wmu_persistent returns 1): fp32 X / M, n_features = 81, k = 4, n_rows a
+ * multiple of 16 whose W fits in LDS (<= ~1.6e6 rows); else 0 and cnmf_wmu_iterations returns
+ * CNMF_ERR_UNSUPPORTED (run cnmf_wmu_sample_pass + cnmf_reduce_partials + cnmf_wmu_basis_update per
+ * iteration).  Buffers as cnmf_wmu_sample_pass's (partials: cnmf_wmu_pass_blocks rows of 2kF;
+ * stage: cnmf_stage_doubles(2kF); counter: cnmf_counter_words(), zero and left zero); AD receives
+ * the last iteration's reduced accumulators, H64 the final basis, W the final W.  A workgroup that
+ * is never co-resident makes the launch give up and set counter[cnmf_counter_err_word()]: the
+ * results are then invalid (the host checks the word).  events: optional 2 recorded events around
+ * the launch (timing). */
+int cnmf_wmu_persistent(int64_t n_rows, int n_features, int k);
+int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                        int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                        int n_features, int k, void* const* events, int n_events, void* stream);
+
 
 /* ---- GPU NNDSVD initialisation (sklearn _initialize_nmf SK:317-373 over
  * randomized_svd, extmath.py:530-604).  The device does the passes over X; the host the F x r

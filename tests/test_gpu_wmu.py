@@ -107,3 +107,106 @@ def test_fully_masked_rows_and_columns():
     assert np.all(W[[0, 77, 1499]] == 0) and np.all(Wr[[0, 77, 1499]] == 0)
     assert np.all(H[:, [5, 80]] == 0) and np.all(Hr[:, [5, 80]] == 0)
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+# ---- the persistent weighted launch (wmu_iter_wt_kernel: fp32, F = 81, k = 4, rows % 16 == 0)
+
+def _oracle_fit(X, M, W0, H0, n_it):
+    return wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                           H0.astype(np.float64), max_iter=n_it, tol=0)
+
+
+@pytest.mark.parametrize("n", [192 * 16, 5008, 65536])
+def test_persistent_matches_oracle(n):
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(n, 81, seed=n, dtype=np.float32)
+    M = _weights(X, n)
+    W0, H0 = random_init(X, 4, 7)
+    plan = _plan(X, M, W0, H0)
+    assert plan.persistent, "fp32 F=81 k=4 rows % 16 == 0 takes the persistent weighted launch"
+    n_it = 100
+    plan.iterate(n_it)
+    plan.check_sync_error()
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = _oracle_fit(X, M, W0, H0, n_it)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+    assert int(plan.counter.abs().sum()) == 0  # tickets and flag left at rest
+
+
+def test_persistent_split_launches_and_repeatable():
+    """n iterations as one launch == as launches of 7 + 13 (the launch boundary carries W and H64
+    only); two runs are bit-identical (no order depends on arrival); the per-iteration kernels
+    agree at the fp32 rounding of their different summation orders."""
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(40000, 81, seed=3, dtype=np.float32)
+    M = _weights(X, 3)
+    W0, H0 = random_init(X, 4, 1)
+    runs = []
+    for split in ([20], [20], [7, 13]):
+        plan = _plan(X, M, W0, H0)
+        assert plan.persistent
+        for n in split:
+            plan.iterate(n)
+        runs.append((plan.W.cpu().numpy(), plan.H64.cpu().numpy()))
+    assert np.array_equal(runs[0][0], runs[1][0]) and np.array_equal(runs[0][1], runs[1][1])
+    assert np.array_equal(runs[0][0], runs[2][0]) and np.array_equal(runs[0][1], runs[2][1])
+    plan = _plan(X, M, W0, H0)
+    plan.persistent = False  # the per-iteration pass + reduce + H-step launches
+    plan.iterate(20)
+    assert rel_fro(plan.W.cpu().numpy(), runs[0][0]) <= 1e-6
+    assert rel_fro(plan.H64.cpu().numpy(), runs[0][1]) <= 1e-6
+
+
+def test_persistent_fully_masked_rows_and_columns():
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1504, 81, seed=21, dtype=np.float32)
+    M = _weights(X, 21)
+    M[[0, 77, 1503], :] = 0.0
+    M[:, [5, 80]] = 0.0
+    W0, H0 = random_init(X, 4, 2)
+    plan = _plan(X, M, W0, H0)
+    assert plan.persistent
+    plan.iterate(40)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = _oracle_fit(X, M, W0, H0, 40)
+    assert np.all(W[[0, 77, 1503]] == 0) and np.all(H[:, [5, 80]] == 0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_persistent_tol_stop_through_api():
+    import cnmf_amd
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(4000, 81, seed=4, dtype=np.float32)
+    M = _weights(X, 4)
+    W0, H0 = random_init(X, 4, 42)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom", tol=1e-3,
+                                 max_iter=400, weights=M)
+    Wr, Hr, nr = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                 H0.astype(np.float64), max_iter=400, tol=1e-3)
+    assert n == nr
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32
+
+
+def test_persistent_full_size():
+    """The bench shape (1e6 x 81, k = 4, 30 % zero weights): 10 iterations against the fp64 oracle
+    and the weighted error non-increasing over the launch boundaries."""
+    import torch
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    n = 1_000_000
+    X = iop_spectra(n, 81, seed=0, dtype=np.float32)
+    M = _weights(X, 0)
+    W0, H0 = random_init(X, 4, 42)
+    plan = _plan(X, M, W0, H0)
+    assert plan.persistent
+    errs = [plan.frobenius_error()]
+    for _ in range(5):
+        plan.iterate(2)
+        plan.check_sync_error()
+        errs.append(plan.frobenius_error())
+    assert all(b <= a * (1 + 1e-12) for a, b in zip(errs, errs[1:])), errs
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    assert np.all(np.isfinite(W)) and np.all(W >= 0) and np.all(H >= 0)
+    del plan
+    torch.cuda.empty_cache()
+    Wr, Hr, _ = _oracle_fit(X, M, W0, H0, 10)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))

@@ -388,6 +388,9 @@ def main():
                  "H-step per launch)")
     elif args.weighted:
         kname = "weighted MU pass (wmu_pass_kernel: W-step + [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))])"
+    elif args.solver == "als" and persistent:
+        kname = ("als_iter_wt_kernel (persistent: K constrained-ALS iterations of W-step pass + in-launch "
+                 "reduction + NNLS H-step per launch)")
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
     elif persistent:

@@ -73,6 +73,9 @@ _SIGS = {
     "cnmf_als_prepare": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _f64, _vp]),
     "cnmf_als_sample_pass": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _f64, _i32, _vp]),
     "cnmf_als_basis_update": (_i32, [_vp, _vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64, _vp]),
+    "cnmf_als_persistent": (_i32, [_i64, _i32, _i32, _i32]),
+    "cnmf_als_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64,
+                                   _i32, _i32, _f64, _f64, _vp, _i32, _vp]),
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                   _i32, _f64, _f64, _f64, _f64, _i32, _vp]),

@@ -3335,13 +3335,19 @@ __device__ double als_L_entry(int F, int a, int b) {  // (DᵀD)[a][b], b >= a, 
   return v;
 }
 
-__global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restrict__ AB, double* __restrict__ H64,
-                                                           double* __restrict__ Ht, double* __restrict__ HHt,
-                                                           double* __restrict__ table, int F, int k, int KP,
-                                                           double lam, double delta2, int do_update) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int t = threadIdx.x;
-  const int V = F + k;
+// The H-step sweep in LDS (als_lds_bytes(F, k) bytes at smem, RED_NT threads): on entry sA [k][F] =
+// WᵀX, sH [k][F] = the basis, sB [k][k] = WᵀW (the first three arrays of the layout); on return
+// sH holds the new basis.  Deterministic: every workgroup that runs it on the same inputs gets the
+// same bits (the LDS atomics only count and take a maximum).
+#ifdef CNMF_STAMPS
+// diagnostic: per H-step call of workgroup 0 (the first 64 calls) and row: BPP iterations, cycles
+__device__ unsigned long long g_hs[64 * 4 * 2];
+__device__ unsigned int g_hs_calls;
+#endif
+__device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, double lam, int t) {
+#ifdef CNMF_STAMPS
+  const unsigned hs_call = blockIdx.x == 0 ? __hip_atomic_load(&g_hs_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 64u;
+#endif
   double* sA = reinterpret_cast<double*>(smem);
   double* sH = sA + (size_t)k * F;
   double* sB = sH + (size_t)k * F;
@@ -3358,17 +3364,14 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
   int* inf = pas + F;
   int* idx = inf + F;
   int* ctl = idx + F;  // [0] n_inf, [1] max infeasible index, [2] mode, [3] n passive
-
-  if (do_update) {
-    for (int e = t; e < k * F; e += RED_NT) {
-      sA[e] = AB[(e / F) * V + (e % F)];
-      sH[e] = H64[e];
-    }
-    for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
-    __syncthreads();
+  {
     for (int j = 0; j < k; ++j) {
       const double bjj = sB[j * k + j];
       if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
+#ifdef CNMF_STAMPS
+      const unsigned long long hs_t0 = __builtin_amdgcn_s_memtime();
+      int hs_iters = 0;
+#endif
       for (int f = t; f < F; f += RED_NT) {
         double b = sA[j * F + f];
         for (int m = 0; m < k; ++m)
@@ -3421,31 +3424,49 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
         __syncthreads();
         if (t == 0) {
           // banded LDLᵀ (unit L, bandwidth 2) fused with the forward solve L z = b, then
-          // x = L⁻ᵀ D⁻¹ z; the recurrences are carried in registers, one division per step
-          double dm1 = 1.0, dm2 = 1.0, im1 = 0.0, im2 = 0.0, l1m1 = 0.0, zm1 = 0.0, zm2 = 0.0;
+          // x = L⁻ᵀ D⁻¹ z; the recurrences are carried in registers, one reciprocal per step.
+          // Since l_{a,a-2}·d_{a-2} = m_{a,a-2}: u1 = m_{a,a-1} − m_{a,a-2}·l_{a-1,a-2} is the
+          // unscaled l_{a,a-1}, and d_a = m_aa − l2·m_{a,a-2} − l1·u1, so the loop-carried cycle is
+          // id_{a-1} -> l1 -> d -> id_a (7 dependent fp64 ops).  The next step's four LDS values are
+          // loaded one step ahead (their latency hides behind that cycle).
+          double im1 = 0.0, im2 = 0.0, l1m1 = 0.0, zm1 = 0.0, zm2 = 0.0;
+          double n_aa = n > 0 ? L0[0] : 1.0, n_a1 = 0.0, n_a2 = 0.0, n_b = n > 0 ? vz[0] : 0.0;
           for (int a = 0; a < n; ++a) {
-            const double m_aa = L0[a], m_a1 = L1[a], m_a2 = L2[a], b = vz[a];
-            const double l2 = m_a2 * im2;                              // l_{a,a-2}
-            const double l1 = (m_a1 - l2 * l1m1 * dm2) * im1;          // l_{a,a-1}
-            const double d = fmax(m_aa - l1 * l1 * dm1 - l2 * l2 * dm2, 1e-300);
-            // 1/d: v_rcp_f64 refined by two Newton steps (full fp64 accuracy) — the IEEE division
-            // sequence sat on this loop's critical path
+            const double m_aa = n_aa, m_a1 = n_a1, m_a2 = n_a2, b = n_b;
+            if (a + 1 < n) {
+              n_aa = L0[a + 1];
+              n_a1 = L1[a + 1];
+              n_a2 = L2[a + 1];
+              n_b = vz[a + 1];
+            }
+            const double l2 = m_a2 * im2;                  // l_{a,a-2}
+            const double u1 = fma(-m_a2, l1m1, m_a1);      // l_{a,a-1}·d_{a-1}
+            const double l1 = u1 * im1;                    // l_{a,a-1}
+            const double d = fmax(fma(-l1, u1, fma(-l2, m_a2, m_aa)), 1e-300);
+            // 1/d: v_rcp_f64 refined by two Newton steps (full fp64 accuracy)
             double id = __builtin_amdgcn_rcp(d);
             id = fma(id, fma(-d, id, 1.0), id);
             id = fma(id, fma(-d, id, 1.0), id);
-            const double z = b - l1 * zm1 - l2 * zm2;
+            const double z = fma(-l2, zm2, fma(-l1, zm1, b));
             L1[a] = l1;
             L2[a] = l2;
             vz[a] = z * id;  // y = D⁻¹ z
-            dm2 = dm1; dm1 = d; im2 = im1; im1 = id; l1m1 = l1; zm2 = zm1; zm1 = z;
+            im2 = im1; im1 = id; l1m1 = l1; zm2 = zm1; zm1 = z;
           }
           double xp1 = 0.0, xp2 = 0.0, l1p1 = 0.0, l2p1 = 0.0, l2p2 = 0.0;
+          double n_y = n > 0 ? vz[n - 1] : 0.0, n_l1 = n > 0 ? L1[n - 1] : 0.0, n_l2 = n > 0 ? L2[n - 1] : 0.0;
           for (int a = n - 1; a >= 0; --a) {
+            const double y = n_y, la1 = n_l1, la2 = n_l2;
+            if (a > 0) {
+              n_y = vz[a - 1];
+              n_l1 = L1[a - 1];
+              n_l2 = L2[a - 1];
+            }
             // x_a = y_a - l_{a+1,a} x_{a+1} - l_{a+2,a} x_{a+2}
-            const double x = vz[a] - l1p1 * xp1 - l2p2 * xp2;
+            const double x = fma(-l2p2, xp2, fma(-l1p1, xp1, y));
             vz[a] = x;
             xp2 = xp1; xp1 = x;
-            l2p2 = l2p1; l2p1 = L2[a]; l1p1 = L1[a];
+            l2p2 = l2p1; l2p1 = la2; l1p1 = la1;
           }
           ctl[0] = 0;
           ctl[1] = -1;
@@ -3484,6 +3505,9 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
         }
         __syncthreads();
         const int mode = ctl[2];
+#ifdef CNMF_STAMPS
+        ++hs_iters;
+#endif
         if (mode == 0) break;
         for (int f = t; f < F; f += RED_NT)
           if ((mode == 1 && inf[f]) || (mode == 2 && f == ctl[1])) pas[f] ^= 1;
@@ -3491,13 +3515,22 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
       }
       for (int f = t; f < F; f += RED_NT) sH[j * F + f] = fmax(vx[f], 0.0);
       __syncthreads();
+#ifdef CNMF_STAMPS
+      if (t == 0 && hs_call < 64u && j < 4) {
+        g_hs[(hs_call * 4 + j) * 2] = (unsigned long long)hs_iters;
+        g_hs[(hs_call * 4 + j) * 2 + 1] = __builtin_amdgcn_s_memtime() - hs_t0;
+      }
+#endif
     }
-    for (int e = t; e < k * F; e += RED_NT) H64[e] = sH[e];
-    __syncthreads();  // workgroup-scope fence + barrier: the H64 stores are visible to this workgroup
   }
-  // Ht / HHt of the (new) H, then the passive-set table of the next W-step
-  basis_update_block(nullptr, H64, Ht, HHt, F, k, KP, 0.0, 0.0, 0, nullptr, reinterpret_cast<double*>(smem));
-  __syncthreads();
+#ifdef CNMF_STAMPS
+  if (t == 0 && blockIdx.x == 0) __hip_atomic_fetch_add(&g_hs_calls, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+// The W-step's passive-set table from HHᵀ (stride KP): per mask (thread t < 16) the inverse of
+// Q_PP, Q = HHᵀ + δ²11ᵀ, by Gauss-Jordan with partial pivoting, scattered to 4x4, and the valid flag
+__device__ void als_table(const double* HHt, int KP, int k, double delta2, double* table, int t) {
   if (t < 16) {
     const int mask = t;
     double T[16];
@@ -3545,6 +3578,33 @@ __global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restr
     for (int e = 0; e < 16; ++e) table[mask * 16 + e] = valid ? T[e] : 0.0;
     table[256 + mask] = valid ? 1.0 : 0.0;
   }
+}
+
+__global__ __launch_bounds__(RED_NT) void als_basis_kernel(const double* __restrict__ AB, double* __restrict__ H64,
+                                                           double* __restrict__ Ht, double* __restrict__ HHt,
+                                                           double* __restrict__ table, int F, int k, int KP,
+                                                           double lam, double delta2, int do_update) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int V = F + k;
+  if (do_update) {
+    double* sA = reinterpret_cast<double*>(smem);
+    double* sH = sA + (size_t)k * F;
+    double* sB = sH + (size_t)k * F;
+    for (int e = t; e < k * F; e += RED_NT) {
+      sA[e] = AB[(e / F) * V + (e % F)];
+      sH[e] = H64[e];
+    }
+    for (int e = t; e < k * k; e += RED_NT) sB[e] = AB[(e / k) * V + F + (e % k)];
+    __syncthreads();
+    als_hstep(smem, F, k, lam, t);
+    for (int e = t; e < k * F; e += RED_NT) H64[e] = sH[e];
+    __syncthreads();  // workgroup-scope fence + barrier: the H64 stores are visible to this workgroup
+  }
+  // Ht / HHt of the (new) H, then the passive-set table of the next W-step
+  basis_update_block(nullptr, H64, Ht, HHt, F, k, KP, 0.0, 0.0, 0, nullptr, reinterpret_cast<double*>(smem));
+  __syncthreads();
+  als_table(HHt, KP, k, delta2, table, t);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -4755,6 +4815,383 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
 }
 
+// ------------------------------------------------------------------------------------------------
+// als_iter_wt_kernel — n constrained-ALS iterations (§8 a7, cfg5; spec oracle/als_ref.py) as ONE
+// persistent launch (fp32 X, F = 81, k = 4).  The wave-tile layout of mu_iter_wt_kernel (one 4-wave
+// workgroup per CU, each wave on its own 16-sample tiles, the next tiles' X prefetched into AGPRs by
+// counted loads), with the W-step of als_pass_sl_kernel and the H-step of als_basis_kernel:
+//   phase 1  c = H·x + δ² in fp64: lane (s, e) forms its 21 features' partials from the fp64 Hᵀ in
+//            LDS; a quad butterfly sums them ((p0 + p1) + (p2 + p3): every lane the same bits, and
+//            the same bits as als_pass_sl_kernel's four feature blocks)
+//   FCLS     lane e evaluates the passive sets e, e + 4, e + 8, e + 12 from the table in LDS; the
+//            least objective among the feasible (ties: lowest mask) by quad shuffles;
+//            w_e = max(T_best·c, 0).  The W-step is exact (it never reads the old W), so W is only
+//            written, once per tile, 256 contiguous bytes per wave
+//   phase 3  A += w'ᵀx, B += w'ᵀw' in fp32 per lane over the iteration (mu_iter_wt_kernel's)
+// End of an iteration: the workgroup's fp64 row [WᵀX | WᵀW], the ticket tree -> AB, and in EVERY
+// workgroup the H-step sweep (als_hstep: deterministic, so every workgroup holds the same bits),
+// then Hᵀ, HHᵀ and the next W-step's table — no broadcast of the new basis.
+// ------------------------------------------------------------------------------------------------
+namespace wa {
+using G4 = wt::Geo<4>;
+constexpr int K = 4, NL = 4, TSW = 16, F = wt::F, NQ = G4::NQ, V = F + K, NOUT = K * V;
+constexpr int NACC = G4::NACC;                                  // NQ·K + K fp32 accumulators
+constexpr int L_STG = 0;                                        // [NWV][XSTR]
+constexpr int L_RED = L_STG + wt::NWV * G4::XSTR;               // [NWV][NL][NACC] fp32
+constexpr int L_H = L_RED + wt::NWV * NL * NACC * 4;            // H fp64 [K][F]
+constexpr int L_AB = L_H + K * F * 8;                           // AB fp64 [K][V]
+constexpr int L_HT = L_AB + NOUT * 8;                           // Hᵀ fp64 [NL·NQ][K], rows >= F zero
+constexpr int L_HHT = L_HT + NL * NQ * K * 8;                   // HHᵀ fp64 [K][K]
+constexpr int L_TAB = L_HHT + K * K * 8;                        // passive-set table (ALS_TAB doubles)
+constexpr int L_FLAG = L_TAB + ALS_TAB * 8;                     // 4 ints
+constexpr int L_HS = (L_FLAG + 16 + 15) / 16 * 16;              // als_hstep's arrays (als_lds_bytes)
+static_assert(L_RED % 16 == 0 && L_HT % 16 == 0 && L_HS % 16 == 0, "16-byte aligned LDS regions");
+static_assert(NOUT * 8 >= wt::NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
+}  // namespace wa
+
+struct AlsPersistArgs {
+  const float* X;
+  float* W;
+  double* H64;       // in: the basis; out: the final basis
+  double* Ht;        // out [F][4] fp64
+  double* HHt;       // out [4][4]
+  double* table;     // out: the next W-step's table
+  double* partials;  // [G][K*V]
+  double* groups;    // [NG][K*V]
+  double* AB;        // [K*V] out: the last iteration's reduced accumulators
+  uint32_t* cnt;     // CNT_WORDS counters (at rest on entry, left at rest)
+  int64_t n_tiles;
+  int n_iter;
+  int n_groups;
+  double delta2;     // sum_to_one²
+  double lam;        // smoothness
+};
+
+// Hᵀ (fp64, the lanes' feature blocks), HHᵀ (fp64; 16 threads per entry, fixed xor tree) and the
+// passive-set table, from the fp64 H in LDS
+__device__ __forceinline__ void wa_derive(unsigned char* smem, int t, double delta2) {
+  using namespace wa;
+  const double* sH = reinterpret_cast<const double*>(smem + L_H);
+  double* sHt = reinterpret_cast<double*>(smem + L_HT);
+  double* sHHt = reinterpret_cast<double*>(smem + L_HHT);
+  for (int e = t; e < NL * NQ * K; e += NT) {
+    const int f = e / K;
+    const int j = e - f * K;
+    sHt[e] = f < F ? sH[j * F + f] : 0.0;
+  }
+  constexpr int TPE = NT / (K * K);
+  const int en = t / TPE, part = t - en * TPE;
+  const int j = en / K, m = en - (en / K) * K;
+  double v = 0.0;
+  for (int f = part; f < F; f += TPE) v = fma(sH[j * F + f], sH[m * F + f], v);
+#pragma unroll
+  for (int o = TPE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (part == 0) sHHt[en] = v;
+  __syncthreads();
+  als_table(sHHt, K, K, delta2, reinterpret_cast<double*>(smem + L_TAB), t);
+  __syncthreads();
+}
+
+// the H-step on AB in LDS: one Gauss-Seidel sweep of exact NNLS rows (als_hstep), then wa_derive.
+// Not inlined: once per iteration, and inlined into each of the main loop's PD body copies it made
+// the loop too large to unroll (the prefetch register sets then went to scratch)
+__device__ __noinline__ void wa_update_basis(int t, double lam, double delta2) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  using namespace wa;
+  double* sH = reinterpret_cast<double*>(smem + L_H);
+  const double* sAB = reinterpret_cast<const double*>(smem + L_AB);
+  double* hA = reinterpret_cast<double*>(smem + L_HS);
+  double* hH = hA + K * F;
+  double* hB = hH + K * F;
+  for (int e = t; e < K * F; e += NT) {
+    hA[e] = sAB[(e / F) * V + (e % F)];
+    hH[e] = sH[e];
+  }
+  if (t < K * K) hB[t] = sAB[(t / K) * V + F + (t % K)];
+  __syncthreads();
+  als_hstep(smem + L_HS, F, K, lam, t);
+  for (int e = t; e < K * F; e += NT) sH[e] = hH[e];
+  __syncthreads();
+  wa_derive(smem, t, delta2);
+}
+
+template <int PD, int OCC>
+__global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
+  using namespace wt;
+  using G4 = Geo<4>;
+  constexpr int KK = wa::K, NL = wa::NL, NQ = wa::NQ, V = wa::V, NOUT = wa::NOUT, NACC = wa::NACC;
+  constexpr int XBW = G4::XBW, XSTR = G4::XSTR, PFW = G4::PFW, LASTL = G4::LASTL;
+  constexpr int PFS = PFW;   // loads per prefetch set: the X tile (W is never read)
+  constexpr int KP = KK / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int s = l / NL, e = l % NL;
+  const int b = blockIdx.x;
+  const int G = gridDim.x;
+  const int NW = NWV * G;
+  const int gw = NWV * b + w;
+  const int NG = a.n_groups;
+  const int g = b % NG;
+  const int gs = (G - g + NG - 1) / NG;
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
+  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);  // this wave's tiles per iteration
+  unsigned char* stg = smem + wa::L_STG + w * XSTR;
+  float* red = reinterpret_cast<float*>(smem + wa::L_RED);
+  double* sH = reinterpret_cast<double*>(smem + wa::L_H);
+  double* sAB = reinterpret_cast<double*>(smem + wa::L_AB);
+  const double* sHtl = reinterpret_cast<const double*>(smem + wa::L_HT) + NQ * e * KK;
+  const double* sTab = reinterpret_cast<const double*>(smem + wa::L_TAB);
+  int* sFlag = reinterpret_cast<int*>(smem + wa::L_FLAG);
+  uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
+  uint32_t* cnt_top = a.cnt + CNT_TOP;
+  uint32_t* flag = a.cnt + CNT_FLAG;
+  uint32_t* err = a.cnt + CNT_ERR;
+
+  // ---- the basis for the first iteration, Hᵀ / HHᵀ / table, the staging pad
+  for (int i = t; i < KK * wa::F; i += NT) sH[i] = a.H64[i];
+  if (l < G4::PADB / 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
+  __syncthreads();
+  wa_derive(smem, t, a.delta2);
+
+  f2 acc[NQ][KP], accB[KP];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int c = 0; c < NQ; ++c)
+#pragma unroll
+      for (int p = 0; p < KP; ++p) acc[c][p] = f2{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < KP; ++p) accB[p] = f2{0.f, 0.f};
+  };
+  zero_acc();
+
+  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile) {
+    const unsigned char* xs = Xb + (size_t)tile * XBW + 16 * l;
+#pragma unroll
+    for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
+    ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS]) {
+    const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
+    stage_rec<0, PFW - 1>(addr, pf);
+    if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
+  };
+
+  const int total = a.n_iter * nbt;
+  u32x4 pf[PD][PFS];
+  // every body stores its W tile (one store): after each of the first PD sets one dummy store (to this
+  // workgroup's partial row, rewritten at the iteration's end) keeps the count of younger operations
+  // at a step's wait exact from the first set on (mu_iter_wt_kernel's streamed-W rule)
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUT) + 64 * w + l;
+#pragma unroll
+  for (int k = 0; k < PD; ++k) {
+    prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+    asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+  }
+  TL_START;
+
+  bool alive = true;
+  int cur_i = 0, cur_it = 0, nx_i = PD;
+  auto step = [&](u32x4 (&pfk)[PFS]) {
+    // younger than this set's loads: the PD - 1 later sets and the W stores of the PD bodies since
+    wait_set<PFS * (PD - 1) + PD, PFS>(pfk);
+    stage(pfk);
+    prefetch(pfk, gw + (int64_t)NW * nx_i);
+    if (++nx_i == nbt) nx_i = 0;
+  };
+  auto body = [&]() {
+    const int it = cur_it, i = cur_i;
+    if (++cur_i == nbt) {
+      cur_i = 0;
+      ++cur_it;
+    }
+    const bool last_it = it + 1 == a.n_iter;
+    const int64_t tile = gw + (int64_t)NW * i;
+    // phase 1: c = H·x over the lane's features in fp64, quad butterfly, + δ²
+    const float* xr = reinterpret_cast<const float*>(stg) + s * wa::F + NQ * e;
+    float xv[NQ];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) xv[c] = xr[c];
+    double cc[KK] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const double2 h01 = *reinterpret_cast<const double2*>(sHtl + c * KK);
+      const double2 h23 = *reinterpret_cast<const double2*>(sHtl + c * KK + 2);
+      const double x = (double)xv[c];
+      cc[0] = fma(x, h01.x, cc[0]);
+      cc[1] = fma(x, h01.y, cc[1]);
+      cc[2] = fma(x, h23.x, cc[2]);
+      cc[3] = fma(x, h23.y, cc[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < KK; ++j) cc[j] += dpp64<0xB1>(cc[j]);  // quad_perm [1,0,3,2]: + lane ^ 1
+#pragma unroll
+    for (int j = 0; j < KK; ++j) cc[j] = cc[j] + dpp64<0x4E>(cc[j]) + a.delta2;  // [2,3,0,1]: + lane ^ 2
+    // FCLS: the passive sets e, e + 4, e + 8, e + 12
+    double bestf = 1.0;
+    int bestm = 16;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = e + 4 * u;
+      const double* T = sTab + m * 16;
+      bool feas = sTab[256 + m] != 0.0;
+      double f = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v = fma(T[r * 4 + q], cc[q], v);
+        feas = feas && v >= 0.0;
+        f = fma(cc[r], v, f);
+      }
+      f *= -0.5;
+      if (feas && (f < bestf || (f == bestf && m < bestm))) {
+        bestf = f;
+        bestm = m;
+      }
+    }
+#pragma unroll
+    for (int off = 1; off <= 2; off <<= 1) {
+      const double of = __shfl_xor(bestf, off);
+      const int om = __shfl_xor(bestm, off);
+      if (of < bestf || (of == bestf && om < bestm)) {
+        bestf = of;
+        bestm = om;
+      }
+    }
+    double wn64 = 0.0;
+    {
+      const double* T = sTab + min(bestm, 15) * 16;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) wn64 = fma(T[e * 4 + q], cc[q], wn64);
+    }
+    const float wn = (float)fmax(wn64, 0.0);
+    a.W[(size_t)tile * (16 * KK) + l] = wn;  // lane l = (s, e): the tile's 256 contiguous bytes
+    // phase 3 with the sample's new row (quad broadcasts)
+    const f2 wp[KP] = {f2{dppf<0x00>(wn), dppf<0x55>(wn)}, f2{dppf<0xAA>(wn), dppf<0xFF>(wn)}};
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      const f2 xx = f2{xv[c], xv[c]};
+#pragma unroll
+      for (int q = 0; q < KP; ++q) acc[c][q] = __builtin_elementwise_fma(xx, wp[q], acc[c][q]);
+    }
+#pragma unroll
+    for (int q = 0; q < KP; ++q) accB[q] = __builtin_elementwise_fma(f2{wn, wn}, wp[q], accB[q]);
+    if (i + 1 != nbt) return;
+
+    // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
+    {
+      float* rw = red + (w * NL + e) * NACC;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        const float4 v = make_float4(sum_over_samples<NL>(acc[c][0].x), sum_over_samples<NL>(acc[c][0].y),
+                                     sum_over_samples<NL>(acc[c][1].x), sum_over_samples<NL>(acc[c][1].y));
+        if (l < NL) *reinterpret_cast<float4*>(rw + c * KK) = v;
+      }
+      const float4 v = make_float4(sum_over_samples<NL>(accB[0].x), sum_over_samples<NL>(accB[0].y),
+                                   sum_over_samples<NL>(accB[1].x), sum_over_samples<NL>(accB[1].y));
+      if (l < NL) *reinterpret_cast<float4*>(rw + NQ * KK) = v;
+    }
+    zero_acc();
+    __syncthreads();
+    {
+      double* prow = a.partials + (size_t)b * NOUT;
+      for (int o = t; o < NOUT; o += NT) {
+        const int j = o / V;
+        const int v = o - j * V;
+        const int ee = v < wa::F ? v / NQ : j;
+        const int idx = v < wa::F ? (v - NQ * ee) * KK + j : NQ * KK + (v - wa::F);
+        const float* rr = red + ee * NACC + idx;
+        constexpr int WS = NL * NACC;
+        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    TL(it, 0);
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
+      sFlag[1] = 0;
+      sFlag[2] = 1;
+    }
+    __syncthreads();
+    if (sFlag[0]) {  // group combiner
+      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
+      }
+      __syncthreads();
+      if (sFlag[1]) {  // top combiner: AB
+        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0 && !last_it)
+          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        TL_PUB(it);
+      }
+    }
+    const bool top = sFlag[1] != 0;
+    if (last_it) {
+      alive = false;
+      if (!top) return;
+      // the last combiner of the launch: the last H-step, then the basis state for the host
+      wa_update_basis(t, a.lam, a.delta2);
+      for (int o = t; o < KK * wa::F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < wa::F * KK; o += NT) a.Ht[o] = reinterpret_cast<const double*>(smem + wa::L_HT)[o];
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + wa::L_HHT)[t];
+      for (int o = t; o < ALS_TAB; o += NT) a.table[o] = sTab[o];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+      if (!sFlag[2]) {
+        alive = false;
+        return;
+      }
+      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      __syncthreads();
+    }
+    wa_update_basis(t, a.lam, a.delta2);
+    TL(it, 1);
+  };
+
+  for (int p = 0; p < total && alive; p += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      step(pf[k]);
+      if (p + k < total && alive) body();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+}
+
 // tile size of the weighted pass: the largest of 64 / 32 / 16 / 8 samples whose LDS fits 64 KB
 static int wmu_tile(int F, int KP) {
   for (int ts = 64; ts >= 8; ts >>= 1) {
@@ -5097,6 +5534,10 @@ int cnmf_debug_timeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * TL_WG * 2 + TL_IT + TL_WG, HIP_SYMBOL(g_tl_hw), sizeof(unsigned int) * TL_WG * 2));
   return CNMF_OK;
 }
+int cnmf_debug_hstep(unsigned long long* host_out) {  // [64 calls][4 rows][BPP iterations, cycles]
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hs), sizeof(unsigned long long) * 64 * 4 * 2));
+  return CNMF_OK;
+}
 int cnmf_debug_xtimeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
   return CNMF_OK;
@@ -5318,6 +5759,81 @@ static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out) {
   if (max_resident(reinterpret_cast<PassFn>(&wmu_iter_wt_kernel<PD>), lds) < G) return false;
   *out = WwLaunch{G, n_tiles, lds};
   return true;
+}
+
+// the persistent constrained-ALS launch for this shape, or false (the per-iteration launches serve it)
+struct WaLaunch {
+  int64_t G, n_tiles;
+  size_t lds;
+};
+// workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2; 2: two waves per SIMD to hide the
+// fp64 and LDS latencies of the W-step, at 256 registers per lane)
+static int wa_occ() {
+  static const int v = getenv("CNMF_ALS_OCC") && atoi(getenv("CNMF_ALS_OCC")) == 2 ? 2 : 1;
+  return v;
+}
+static PassFn wa_fn() {
+  return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1>)
+                       : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 2>);
+}
+static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out) {
+  constexpr int PD = 3;
+  if (x_dtype != CNMF_F32 || F != wt::F || k != wa::K || n_rows <= 0 || n_rows % wa::TSW != 0) return false;
+  if (getenv("CNMF_ALS_PERSIST") && atoi(getenv("CNMF_ALS_PERSIST")) == 0) return false;
+  const int64_t n_tiles = n_rows / wa::TSW;
+  const int64_t G = std::min<int64_t>({(int64_t)device_cus() * wa_occ(), n_tiles / (wt::NWV * (PD + 1)),
+                                       (int64_t)sl::GROUP * sl::MAX_GROUPS});
+  if (G < 1) return false;
+  const size_t lds = (size_t)wa::L_HS + als_lds_bytes(F, k);
+  if (lds > kMaxLds) return false;
+  if (max_resident(wa_fn(), lds) < G) return false;
+  *out = WaLaunch{G, n_tiles, lds};
+  return true;
+}
+
+int cnmf_als_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
+  WaLaunch L;
+  return wa_plan(n_rows, x_dtype, n_features, k, &L) ? 1 : 0;
+}
+
+int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                        double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                        double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
+                        void* const* events, int n_events, void* stream) {
+  if (n_iter <= 0) return CNMF_OK;
+  WaLaunch L;
+  if (!wa_plan(n_rows, x_dtype, n_features, k, &L))
+    return set_err(CNMF_ERR_UNSUPPORTED, "the persistent constrained ALS serves fp32 F=81 k=4 with rows a multiple "
+                   "of 16 (n_rows=%lld F=%d k=%d)", (long long)n_rows, n_features, k);
+  if (!X || !W || !H64 || !Ht || !HHt || !table || !partials || !stage || !counter || !AB)
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+    return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+  if (!(sum_to_one >= 0.0) || !(smoothness >= 0.0)) return set_err(CNMF_ERR_ARG, "smoothness and sum_to_one must be >= 0");
+  if (L.G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
+                                    (long long)n_parts, (long long)L.G);
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  AlsPersistArgs pa;
+  pa.X = static_cast<const float*>(X);
+  pa.W = static_cast<float*>(W);
+  pa.H64 = H64;
+  pa.Ht = Ht;
+  pa.HHt = HHt;
+  pa.table = table;
+  pa.partials = partials;
+  pa.groups = stage;
+  pa.AB = AB;
+  pa.cnt = counter;
+  pa.n_tiles = L.n_tiles;
+  pa.n_iter = n_iter;
+  pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  pa.delta2 = sum_to_one * sum_to_one;
+  pa.lam = smoothness;
+  void* args[] = {&pa};
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn()), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+  return CNMF_OK;
 }
 
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,

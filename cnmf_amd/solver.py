@@ -451,14 +451,17 @@ class ALSPlan(MUPlan):
         super().__init__(X, n_components, group=group)
         if self.k > 4:
             raise _lib.HipLibraryError(f"constrained ALS supports n_components <= 4 (got {self.k})")
-        self.persistent = False  # the persistent kernel runs the MU update only
-        self.persistent_shape = False
         self.delta = float(sum_to_one or 0.0)
         self.lam = float(smoothness or 0.0)
         if self.delta < 0 or self.lam < 0:
             raise ValueError("sum_to_one and smoothness must be >= 0")
         self.table = torch.zeros(int(self.lib.cnmf_als_table_doubles()), dtype=torch.float64,
                                  device=self.device)
+        with torch.cuda.device(self.device):
+            p = self.lib.cnmf_als_persistent(self.n_rows, self.F, self.k, self.xdt)
+        # one persistent launch per stretch of iterations (als_iter_wt_kernel), single GPU
+        self.persistent_shape = bool(check(p, "cnmf_als_persistent"))
+        self.persistent = self.persistent_shape and self.world == 1
 
     def refresh_basis(self):
         with torch.cuda.device(self.device):
@@ -479,7 +482,29 @@ class ALSPlan(MUPlan):
                 _ptr(self.AB), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt), _ptr(self.table),
                 self.F, self.k, self.lam, self.delta, self._stream()), "cnmf_als_basis_update")
 
+    def describe(self) -> str:
+        if self.persistent:
+            return ("als_iter_wt_kernel<PD=3>: wave tiles of 16 samples, one 4-wave workgroup per CU, "
+                    "in-launch reduction and H-step (every workgroup)")
+        return "ALS W-step pass + cnmf_reduce_partials + als_basis_kernel per iteration"
+
+    def tune(self, *args, **kwargs) -> dict:
+        return {}  # one layout
+
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
+        """n_iter ALS iterations; pass_events: 2 events around the one launch when self.persistent,
+        else 2·n_iter events around each W-step pass."""
+        if n_iter <= 0:
+            return
+        if self.persistent and update_H:
+            with torch.cuda.device(self.device):
+                check(self.lib.cnmf_als_iterations(
+                    n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
+                    _ptr(self.HHt), _ptr(self.table), _ptr(self.partials), self.n_parts,
+                    _ptr(self.stage), _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
+                    self.delta, self.lam, *_event_array(pass_events), self._stream()),
+                    "cnmf_als_iterations")
+            return
         ev = list(pass_events) if pass_events is not None else None
         stream = torch.cuda.current_stream(self.device) if ev is not None else None
         for i in range(max(n_iter, 0)):

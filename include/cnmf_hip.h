@@ -211,6 +211,20 @@ int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, 
 int cnmf_als_basis_update(const double* AB, double* H64, double* Ht, double* HHt, double* table,
                           int n_features, int k, double smoothness, double sum_to_one, void* stream);
 
+/* n constrained-ALS iterations (W-step, [WᵀX | WᵀW], H-step) as ONE persistent launch
+ * (als_iter_wt_kernel).  Served shape (cnmf_als_persistent returns 1): fp32 X, n_features = 81,
+ * k = 4, n_rows a multiple of 16; else 0 and cnmf_als_iterations returns CNMF_ERR_UNSUPPORTED (run
+ * cnmf_als_sample_pass + cnmf_reduce_partials + cnmf_als_basis_update per iteration).  The W-step
+ * reads H64 (and derives Ht / HHt / the table itself); on return H64, Ht, HHt and table hold the
+ * final basis state, W the last W-step, AB the last iteration's reduced accumulators.  Buffers as
+ * cnmf_mu_iterations'; a workgroup that is never co-resident makes the launch give up and set
+ * counter[cnmf_counter_err_word()] (results then invalid).  events: optional 2 recorded events. */
+int cnmf_als_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
+int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                        double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                        double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
+                        void* const* events, int n_events, void* stream);
+
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);

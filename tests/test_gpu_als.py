@@ -135,3 +135,57 @@ def test_als_full_size_properties():
     W = outs[0][0].double()
     assert bool((W >= 0).all())
     assert float((W.sum(1) - 1).abs().mean()) < 0.05
+
+
+# ---- the persistent constrained-ALS launch (als_iter_wt_kernel: fp32, F = 81, k = 4, rows % 16 == 0)
+
+@pytest.mark.parametrize("delta, lam", [(0.0, 0.0), (1.0, 0.5), (3.0, 5.0)])
+def test_persistent_als_matches_oracle(delta, lam):
+    X, W0, H0 = _data(3008, 81, 4, seed=11)
+    plan = _plan(X, W0, H0, delta, lam)
+    assert plan.persistent, "fp32 F=81 k=4 rows % 16 == 0 takes the persistent ALS launch"
+    plan.iterate(30)
+    plan.check_sync_error()
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                max_iter=30, tol=0.0, sum_to_one=delta, smoothness=lam)
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+    assert plan.counters_at_rest()
+    # the basis state the launch leaves for the per-iteration kernels (Hᵀ, HHᵀ)
+    np.testing.assert_allclose(plan.Ht.cpu().numpy()[:, :4], H.T, rtol=0, atol=0)
+    np.testing.assert_allclose(plan.HHt.cpu().numpy(), H @ H.T, rtol=1e-12)
+
+
+def test_persistent_als_split_launches_and_per_iteration_path():
+    """20 iterations as one launch == 7 + 13 (bit for bit: only W and H64 cross a launch boundary,
+    Hᵀ / HHᵀ / the table are derived in-launch); two runs bit-identical; the per-iteration kernels
+    agree to their different fp32 summation orders of WᵀX."""
+    X, W0, H0 = _mixtures(40000, 81, 4, seed=5)
+    runs = []
+    for split in ([20], [20], [7, 13]):
+        plan = _plan(X, W0, H0, 1.0, 0.5)
+        assert plan.persistent
+        for n in split:
+            plan.iterate(n)
+        runs.append((plan.W.cpu().numpy(), plan.H64.cpu().numpy()))
+    for r in runs[1:]:
+        assert np.array_equal(runs[0][0], r[0]) and np.array_equal(runs[0][1], r[1])
+    plan = _plan(X, W0, H0, 1.0, 0.5)
+    plan.persistent = False
+    plan.iterate(20)
+    # the first W-step is bit-identical (same c = H·x bits); later ones see H from differently
+    # ordered fp32 sums of WᵀX (~1e-8), amplified by cond(Q_PP) of these near-collinear endmembers
+    assert rel_fro(plan.W.cpu().numpy(), runs[0][0]) <= 1e-5
+    assert rel_fro(plan.H64.cpu().numpy(), runs[0][1]) <= 1e-5
+
+
+def test_persistent_als_tol_stop_matches_oracle():
+    import cnmf_amd
+    X, W0, H0 = _data(2000, 81, 4, seed=12)
+    W, H, n = cnmf_amd.factorise(X, W0.copy(), H0.copy(), n_components=4, init="custom",
+                                 solver="als", sum_to_one=1.0, smoothness=0.1, tol=1e-3,
+                                 max_iter=200)
+    Wr, Hr, nr = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                 max_iter=200, tol=1e-3, sum_to_one=1.0, smoothness=0.1)
+    assert n == nr
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5

@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1000, help="iterations before the stamped launch (clock ramp)")
+    ap.add_argument("--solver", default="mu", choices=["mu", "als", "wmu"],
+                    help="als: the persistent constrained ALS (sum_to_one 1, smoothness 0.5); wmu: the "
+                         "persistent weighted MU (30 %% zero weights)")
     ap.add_argument("--exchange", action="store_true",
                     help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
     a = ap.parse_args()
@@ -47,7 +50,16 @@ def main():
             port = so.getsockname()[1]
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         group = dist.group.WORLD
-    plan = MUPlan(torch.from_numpy(X).cuda(), a.k, group=group)
+    if a.solver == "als":
+        from cnmf_amd.solver import ALSPlan
+        plan = ALSPlan(torch.from_numpy(X).cuda(), a.k, sum_to_one=1.0, smoothness=0.5)
+    elif a.solver == "wmu":
+        from cnmf_amd.solver import WeightedMUPlan
+        rng = np.random.default_rng(0)
+        M = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)
+        plan = WeightedMUPlan(torch.from_numpy(X).cuda(), torch.from_numpy(M).cuda(), a.k)
+    else:
+        plan = MUPlan(torch.from_numpy(X).cuda(), a.k, group=group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     if a.exchange:
@@ -136,6 +148,16 @@ def main():
             "slot_loads_sum": round(float(np.median(x[:, 3] - x[:, 2])) * 10 / 1e3, 2),
             "to_publish": round(float(np.median(p_ - x[:, 3])) * 10 / 1e3, 2),
             "arrival_to_start": round(float(np.median(x[:, 0] - arr[1:n - 1].max(axis=1))) * 10 / 1e3, 2)}
+    if a.solver == "als":  # H-step of workgroup 0: BPP iterations and cycles per row, per call
+        fh = lib.cnmf_debug_hstep
+        fh.argtypes = [ctypes.c_void_p]
+        fh.restype = ctypes.c_int
+        hb = np.zeros(64 * 4 * 2, dtype=np.uint64)
+        _lib.check(fh(hb.ctypes.data), "hstep")
+        hs = hb.reshape(64, 4, 2).astype(np.int64)
+        used = hs[:, :, 1].sum(axis=1) > 0
+        summary["hstep_bpp_iters_per_row_last_calls"] = hs[used][-5:, :, 0].tolist()
+        summary["hstep_kcycles_per_row_last_calls"] = (hs[used][-5:, :, 1] / 1e3).round(1).tolist()
     print(json.dumps(summary), flush=True)
     for r in rows[:5]:
         print(json.dumps({k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}), flush=True)

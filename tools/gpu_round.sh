@@ -16,4 +16,6 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_drive
 $P --pmc FETCH_SIZE -d gpurun_out/pmc/fetch -o fetch -- python3 tools/prof_pass.py > gpurun_out/pmc/fetch.log 2>&1 &&
 $P --pmc WRITE_SIZE -d gpurun_out/pmc/write -o write -- python3 tools/prof_pass.py > gpurun_out/pmc/write.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 500 --warmup 500 --no-cpu > gpurun_out/prof.log 2>&1
-echo "exit=$?"
+rc=$?
+echo "exit=$rc"
+exit $rc

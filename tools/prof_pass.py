@@ -16,6 +16,8 @@ def main():
     ap.add_argument("--k", type=int, default=4)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    ap.add_argument("--solver", default="mu", choices=["mu", "als"],
+                    help="als: the persistent constrained ALS (sum_to_one 1, smoothness 0.5)")
     a = ap.parse_args()
     import torch
     from cnmf_amd.solver import MUPlan
@@ -25,7 +27,11 @@ def main():
     Xd = torch.from_numpy(X).cuda()
     if a.dtype == "bf16":
         Xd = Xd.to(torch.bfloat16)
-    plan = MUPlan(Xd, a.k)
+    if a.solver == "als":
+        from cnmf_amd.solver import ALSPlan
+        plan = ALSPlan(Xd, a.k, sum_to_one=1.0, smoothness=0.5)
+    else:
+        plan = MUPlan(Xd, a.k)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     plan.iterate(a.iters)

@@ -3344,7 +3344,7 @@ __device__ double als_L_entry(int F, int a, int b) {  // (DᵀD)[a][b], b >= a, 
 __device__ unsigned long long g_hs[64 * 4 * 2];
 __device__ unsigned int g_hs_calls;
 #endif
-__device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, double lam, int t) {
+__device__ __forceinline__ void als_hstep_block(unsigned char* smem, int F, int k, double lam, int t) {
 #ifdef CNMF_STAMPS
   const unsigned hs_call = blockIdx.x == 0 ? __hip_atomic_load(&g_hs_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 64u;
 #endif
@@ -3528,54 +3528,274 @@ __device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, dou
 #endif
 }
 
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// The same sweep for F <= 128 on ONE wave, without a workgroup barrier inside it (same LDS layout;
+// the other waves wait at the closing barrier).  Lane l holds features l and l + 64 in registers;
+// the passive set is compressed by ballots, and each solve M_PP x = b_P is a parallel cyclic
+// reduction over 2x2 blocks of the compressed pentadiagonal system (log2(n/2) steps of register
+// arithmetic and lane shuffles) instead of the n sequential steps of a banded LDLᵀ, whose
+// loop-carried chain of ~10 dependent fp64 operations made a row cost 20-40 k cycles
+// (profiles/r02/session5/als_diag).  LDS is only used for gathers and neighbour reads, in program
+// order inside the wave.
+__device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k, double lam, int t) {
+#ifdef CNMF_STAMPS
+  const unsigned hs_call = blockIdx.x == 0 ? __hip_atomic_load(&g_hs_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 64u;
+#endif
+  if (t < 64) {
+    const int lane = t;
+    double* sA = reinterpret_cast<double*>(smem);
+    double* sH = sA + (size_t)k * F;
+    double* sB = sH + (size_t)k * F;
+    double* vb = sB + k * k;
+    double* vx = vb + F;
+    double* d0 = vx + F;
+    double* e1 = d0 + F;
+    double* e2 = e1 + F;
+    double* vz = e2 + 4 * F;  // the block form's L0, L1, L2 are not used here
+    int* idx = reinterpret_cast<int*>(vz + F) + 2 * F;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int j = 0; j < k; ++j) {
+      const double bjj = sB[j * k + j];
+      if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
+#ifdef CNMF_STAMPS
+      const unsigned long long hs_t0 = __builtin_amdgcn_s_memtime();
+      int hs_iters = 0;
+#endif
+      double rb[2], rd[2], re1[2], re2[2], xf[2];
+      bool pas[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int f = lane + 64 * c;
+        rb[c] = 0.0; rd[c] = 1.0; re1[c] = 0.0; re2[c] = 0.0; xf[c] = 0.0;
+        pas[c] = false;
+        if (f < F) {
+          double b = sA[j * F + f];
+          for (int m = 0; m < k; ++m)
+            if (m != j) b -= sB[j * k + m] * sH[m * F + f];
+          rb[c] = b;
+          rd[c] = bjj + lam * als_L_entry(F, f, f);
+          re1[c] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
+          re2[c] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
+          pas[c] = sH[j * F + f] > 0.0;
+          vb[f] = rb[c];
+          d0[f] = rd[c];
+          e1[f] = re1[c];
+          e2[f] = re2[c];
+        }
+      }
+      int alpha = 3, beta = F + 1;  // BPP control (wave-uniform)
+      for (int iter = 0; iter < 5 * F + 10; ++iter) {
+        // ---- compress the passive set: idx[pos] = feature
+        const uint64_t bal0 = __ballot(pas[0]), bal1 = __ballot(pas[1]);
+        const int n0 = __popcll(bal0), n = n0 + __popcll(bal1);
+        const int pos[2] = {(int)__popcll(bal0 & lt), n0 + (int)__popcll(bal1 & lt)};
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (pas[c]) idx[pos[c]] = lane + 64 * c;
+        lds_order();
+        // ---- M_PP x = b_P by parallel cyclic reduction on 2x2 blocks (lane i = compressed rows
+        // 2i, 2i+1; nb = ceil(n/2) <= 64 blocks; log2(nb) steps instead of n sequential LDLᵀ
+        // steps).  The pentadiagonal M_PP is block tridiagonal: A_i (rows 2i, 2i+1 x columns 2i-2,
+        // 2i-1), B_i (symmetric), C_i = A_{i+1}ᵀ.  Step s eliminates blocks i +- s:
+        //   B_i -= A_i B_{i-s}⁻¹ A_iᵀ + C_i B_{i+s}⁻¹ C_iᵀ,  A_i <- -A_i B_{i-s}⁻¹ A_{i-s},
+        //   d_i -= A_i B_{i-s}⁻¹ d_{i-s} + C_i B_{i+s}⁻¹ d_{i+s},  with C_i = A_{i+s}ᵀ at every
+        // stride (the reduced systems are Schur complements of a symmetric matrix).  Positions >= n
+        // are identity rows with zero coupling; blocks outside the wave contribute zero.
+        {
+          // compressed entry of position p: M_pp, M_p,p-1, M_p,p-2, b_p
+          auto ent = [&](int p, double& m0, double& m1, double& m2, double& z) {
+            m0 = 1.0; m1 = 0.0; m2 = 0.0; z = 0.0;
+            if (p < n) {
+              const int fp = idx[p];
+              m0 = d0[fp];
+              m1 = p >= 1 ? als_m_low(e1, e2, fp, idx[p - 1]) : 0.0;
+              m2 = p >= 2 ? als_m_low(e1, e2, fp, idx[p - 2]) : 0.0;
+              z = vb[fp];
+            }
+          };
+          const int nb = (n + 1) >> 1;
+          double p0m0, p0m1, p0m2, p0z, p1m0, p1m1, p1m2, p1z;
+          ent(2 * lane, p0m0, p0m1, p0m2, p0z);
+          ent(2 * lane + 1, p1m0, p1m1, p1m2, p1z);
+          double b00 = p0m0, b01 = p1m1, b11 = p1m0;
+          double a00 = p0m2, a01 = p0m1, a10 = 0.0, a11 = p1m2;
+          double r0 = p0z, r1 = p1z;
+          auto inv2 = [](double x00, double x01, double x11, double& i00, double& i01, double& i11) {
+            const double det = fmax(fma(x00, x11, -x01 * x01), 1e-300);
+            double id = __builtin_amdgcn_rcp(det);
+            id = fma(id, fma(-det, id, 1.0), id);
+            id = fma(id, fma(-det, id, 1.0), id);
+            i00 = x11 * id;
+            i11 = x00 * id;
+            i01 = -x01 * id;
+          };
+          for (int st = 1; st < nb; st <<= 1) {
+            double i00, i01, i11;
+            inv2(b00, b01, b11, i00, i01, i11);
+            const bool hl = lane >= st, hr = lane + st < 64;
+            const int sl_ = hl ? lane - st : lane, sr_ = hr ? lane + st : lane;
+            auto from = [&](double v, int src, bool ok) { const double u = __shfl(v, src, 64); return ok ? u : 0.0; };
+            const double Li00 = from(i00, sl_, hl), Li01 = from(i01, sl_, hl), Li11 = from(i11, sl_, hl);
+            const double La00 = from(a00, sl_, hl), La01 = from(a01, sl_, hl), La10 = from(a10, sl_, hl),
+                         La11 = from(a11, sl_, hl), Lr0 = from(r0, sl_, hl), Lr1 = from(r1, sl_, hl);
+            const double Ri00 = from(i00, sr_, hr), Ri01 = from(i01, sr_, hr), Ri11 = from(i11, sr_, hr);
+            const double c00 = from(a00, sr_, hr), c10 = from(a01, sr_, hr), c01 = from(a10, sr_, hr),
+                         c11 = from(a11, sr_, hr), Rr0 = from(r0, sr_, hr), Rr1 = from(r1, sr_, hr);
+            // T = A_i B_{i-s}⁻¹, U = C_i B_{i+s}⁻¹
+            const double t00 = fma(a00, Li00, a01 * Li01), t01 = fma(a00, Li01, a01 * Li11);
+            const double t10 = fma(a10, Li00, a11 * Li01), t11 = fma(a10, Li01, a11 * Li11);
+            const double u00 = fma(c00, Ri00, c01 * Ri01), u01 = fma(c00, Ri01, c01 * Ri11);
+            const double u10 = fma(c10, Ri00, c11 * Ri01), u11 = fma(c10, Ri01, c11 * Ri11);
+            b00 = b00 - fma(t00, a00, t01 * a01) - fma(u00, c00, u01 * c01);
+            b01 = b01 - fma(t00, a10, t01 * a11) - fma(u00, c10, u01 * c11);
+            b11 = b11 - fma(t10, a10, t11 * a11) - fma(u10, c10, u11 * c11);
+            const double n00 = -fma(t00, La00, t01 * La10), n01 = -fma(t00, La01, t01 * La11);
+            const double n10 = -fma(t10, La00, t11 * La10), n11 = -fma(t10, La01, t11 * La11);
+            a00 = n00; a01 = n01; a10 = n10; a11 = n11;
+            const double q0 = r0 - fma(t00, Lr0, t01 * Lr1) - fma(u00, Rr0, u01 * Rr1);
+            const double q1 = r1 - fma(t10, Lr0, t11 * Lr1) - fma(u10, Rr0, u11 * Rr1);
+            r0 = q0;
+            r1 = q1;
+          }
+          double i00, i01, i11;
+          inv2(b00, b01, b11, i00, i01, i11);
+          if (2 * lane < n) vz[2 * lane] = fma(i00, r0, i01 * r1);
+          if (2 * lane + 1 < n) vz[2 * lane + 1] = fma(i01, r0, i11 * r1);
+        }
+        lds_order();
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int f = lane + 64 * c;
+          xf[c] = pas[c] ? vz[pos[c]] : 0.0;
+          if (f < F) vx[f] = xf[c];
+        }
+        lds_order();
+        bool bad[2];
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int f = lane + 64 * c;
+          bad[c] = false;
+          if (f < F) {
+            const double x = xf[c];
+            if (pas[c]) {
+              bad[c] = x < 0.0;
+            } else {
+              double y = rd[c] * x - rb[c];
+              if (f + 1 < F) y += re1[c] * vx[f + 1];
+              if (f >= 1) y += e1[f - 1] * vx[f - 1];
+              if (f + 2 < F) y += re2[c] * vx[f + 2];
+              if (f >= 2) y += e2[f - 2] * vx[f - 2];
+              bad[c] = y < 0.0;
+            }
+          }
+        }
+        const uint64_t bb0 = __ballot(bad[0]), bb1 = __ballot(bad[1]);
+        const int ninf = __popcll(bb0) + __popcll(bb1);
+        const int maxbad = bb1 ? 64 + 63 - __clzll(bb1) : (bb0 ? 63 - __clzll(bb0) : -1);
+        int mode;
+        if (ninf == 0) mode = 0;
+        else if (ninf < beta) { beta = ninf; alpha = 3; mode = 1; }
+        else if (alpha >= 1) { --alpha; mode = 1; }
+        else mode = 2;
+#ifdef CNMF_STAMPS
+        ++hs_iters;
+#endif
+        if (mode == 0) break;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if ((mode == 1 && bad[c]) || (mode == 2 && lane + 64 * c == maxbad)) pas[c] = !pas[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (lane + 64 * c < F) sH[j * F + lane + 64 * c] = fmax(xf[c], 0.0);
+      lds_order();
+#ifdef CNMF_STAMPS
+      if (lane == 0 && hs_call < 64u && j < 4) {
+        g_hs[(hs_call * 4 + j) * 2] = (unsigned long long)hs_iters;
+        g_hs[(hs_call * 4 + j) * 2 + 1] = __builtin_amdgcn_s_memtime() - hs_t0;
+      }
+#endif
+    }
+  }
+  __syncthreads();
+#ifdef CNMF_STAMPS
+  if (t == 0 && blockIdx.x == 0) __hip_atomic_fetch_add(&g_hs_calls, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+
+// the H-step sweep: one wave for F <= 128, else the workgroup form
+__device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, double lam, int t) {
+  if (F <= 128) als_hstep_wave(smem, F, k, lam, t);
+  else als_hstep_block(smem, F, k, lam, t);
+}
+
 // The W-step's passive-set table from HHᵀ (stride KP): per mask (thread t < 16) the inverse of
 // Q_PP, Q = HHᵀ + δ²11ᵀ, by Gauss-Jordan with partial pivoting, scattered to 4x4, and the valid flag
 __device__ void als_table(const double* HHt, int KP, int k, double delta2, double* table, int t) {
+  // Register-resident form (every index compile-time; the runtime-indexed compressed arrays went to
+  // scratch): Gauss-Jordan on the full 4x4 [Q | I] with the rows / columns outside P held at the
+  // identity.  The entries of P see exactly the compressed elimination's operations in the same
+  // order (the pivot search runs over P's rows in ascending order, strict >, as the compressed
+  // search does; rows outside P are never touched by an elimination step of a P column and vice
+  // versa), so the table is the same bits as the compressed form's.
   if (t < 16) {
     const int mask = t;
-    double T[16];
-    for (int e = 0; e < 16; ++e) T[e] = 0.0;
-    bool valid = (mask >> k) == 0 || k >= 4;
-    if (k < 4 && (mask >> k) != 0) valid = false;
-    int P[4], n = 0;
-    for (int j = 0; j < 4; ++j)
-      if (mask >> j & 1) P[n++] = j;
-    if (valid && n > 0) {
-      double a[4][8];
-      double dmax = 0.0;
-      for (int r = 0; r < n; ++r)
-        for (int c = 0; c < n; ++c) {
-          a[r][c] = HHt[P[r] * KP + P[c]] + delta2;
-          a[r][4 + c] = r == c ? 1.0 : 0.0;
-          if (r == c) dmax = fmax(dmax, fabs(a[r][c]));
-        }
-      for (int c = 0; c < n && valid; ++c) {
-        int piv = c;
-        for (int r = c + 1; r < n; ++r)
-          if (fabs(a[r][c]) > fabs(a[piv][c])) piv = r;
-        if (!(fabs(a[piv][c]) > 1e-13 * dmax)) {
-          valid = false;
-          break;
-        }
-        if (piv != c)
-          for (int e = 0; e < 8; ++e) {
-            const double tmp = a[c][e];
-            a[c][e] = a[piv][e];
-            a[piv][e] = tmp;
-          }
-        const double inv = 1.0 / a[c][c];
-        for (int e = 0; e < 8; ++e) a[c][e] *= inv;
-        for (int r = 0; r < n; ++r) {
-          if (r == c) continue;
-          const double fct = a[r][c];
-          for (int e = 0; e < 8; ++e) a[r][e] -= fct * a[c][e];
+    bool valid = !(k < 4 && (mask >> k) != 0);
+    double a[4][8];
+    double dmax = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool in = (mask >> r & 1) && (mask >> c & 1);
+        const double q = (r < k && c < k) ? HHt[r * KP + c] + delta2 : 0.0;
+        a[r][c] = in ? q : (r == c ? 1.0 : 0.0);
+        a[r][4 + c] = r == c ? 1.0 : 0.0;
+        if (in && r == c) dmax = fmax(dmax, fabs(q));
+      }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (!(mask >> c & 1)) continue;  // identity column: nothing to eliminate
+      // pivot: the P row r >= c of largest |a[r][c]| (first on ties)
+      int piv = c;
+      double pv = fabs(a[c][c]);
+#pragma unroll
+      for (int r = c + 1; r < 4; ++r) {
+        const bool take = (mask >> r & 1) && fabs(a[r][c]) > pv;
+        piv = take ? r : piv;
+        pv = take ? fabs(a[r][c]) : pv;
+      }
+      valid = valid && pv > 1e-13 * dmax;
+      // swap rows c and piv (selects)
+#pragma unroll
+      for (int r = c + 1; r < 4; ++r) {
+        const bool sw = piv == r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double tc = a[c][e], tr = a[r][e];
+          a[c][e] = sw ? tr : tc;
+          a[r][e] = sw ? tc : tr;
         }
       }
-      if (valid)
-        for (int r = 0; r < n; ++r)
-          for (int c = 0; c < n; ++c) T[P[r] * 4 + P[c]] = a[r][4 + c];
+      const double inv = 1.0 / a[c][c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[c][e] *= inv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (r == c || !(mask >> r & 1)) continue;
+        const double fct = a[r][c];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[r][e] -= fct * a[c][e];
+      }
     }
-    for (int e = 0; e < 16; ++e) table[mask * 16 + e] = valid ? T[e] : 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bool in = (mask >> r & 1) && (mask >> c & 1);
+        table[mask * 16 + r * 4 + c] = (valid && in) ? a[r][4 + c] : 0.0;
+      }
     table[256 + mask] = valid ? 1.0 : 0.0;
   }
 }
@@ -4892,10 +5112,9 @@ __device__ __forceinline__ void wa_derive(unsigned char* smem, int t, double del
   __syncthreads();
 }
 
-// the H-step on AB in LDS: one Gauss-Seidel sweep of exact NNLS rows (als_hstep), then wa_derive.
-// Not inlined: once per iteration, and inlined into each of the main loop's PD body copies it made
-// the loop too large to unroll (the prefetch register sets then went to scratch)
-__device__ __noinline__ void wa_update_basis(int t, double lam, double delta2) {
+// the H-step on AB in LDS: one Gauss-Seidel sweep of exact NNLS rows (als_hstep), then wa_derive
+// (inlined once, after the kernel's streaming loop)
+__device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using namespace wa;
   double* sH = reinterpret_cast<double*>(smem + L_H);
@@ -4978,7 +5197,6 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
   };
 
-  const int total = a.n_iter * nbt;
   u32x4 pf[PD][PFS];
   // every body stores its W tile (one store): after each of the first PD sets one dummy store (to this
   // workgroup's partial row, rewritten at the iteration's end) keeps the count of younger operations
@@ -4992,21 +5210,21 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   TL_START;
 
   bool alive = true;
-  int cur_i = 0, cur_it = 0, nx_i = PD;
+  // steps per iteration: the wave's nbt tiles padded to a multiple of PD, so that every iteration
+  // starts on register set 0 and the end-of-iteration code (reduction, H-step) is emitted ONCE,
+  // inlined under the kernel's register budget, after the unrolled streaming loop.  A pad step
+  // re-loads the wave's first tile into its set and stores one dummy word (the step's wait counts
+  // one store per step).
+  const int nbp = (nbt + PD - 1) / PD * PD;
+  int nx_i = PD;  // step (within its iteration) whose tile the next prefetch loads
   auto step = [&](u32x4 (&pfk)[PFS]) {
-    // younger than this set's loads: the PD - 1 later sets and the W stores of the PD bodies since
+    // younger than this set's loads: the PD - 1 later sets and the stores of the PD steps since
     wait_set<PFS * (PD - 1) + PD, PFS>(pfk);
     stage(pfk);
-    prefetch(pfk, gw + (int64_t)NW * nx_i);
-    if (++nx_i == nbt) nx_i = 0;
+    prefetch(pfk, gw + (int64_t)NW * (nx_i < nbt ? nx_i : 0));
+    if (++nx_i == nbp) nx_i = 0;
   };
-  auto body = [&]() {
-    const int it = cur_it, i = cur_i;
-    if (++cur_i == nbt) {
-      cur_i = 0;
-      ++cur_it;
-    }
-    const bool last_it = it + 1 == a.n_iter;
+  auto wbody = [&](int i) {
     const int64_t tile = gw + (int64_t)NW * i;
     // phase 1: c = H·x over the lane's features in fp64, quad butterfly, + δ²
     const float* xr = reinterpret_cast<const float*>(stg) + s * wa::F + NQ * e;
@@ -5078,8 +5296,9 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
 #pragma unroll
     for (int q = 0; q < KP; ++q) accB[q] = __builtin_elementwise_fma(f2{wn, wn}, wp[q], accB[q]);
-    if (i + 1 != nbt) return;
-
+  };
+  auto end_iteration = [&](int it) {
+    const bool last_it = it + 1 == a.n_iter;
     // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
     {
       float* rw = red + (w * NL + e) * NACC;
@@ -5182,12 +5401,16 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     TL(it, 1);
   };
 
-  for (int p = 0; p < total && alive; p += PD) {
+  for (int it = 0; it < a.n_iter && alive; ++it) {
+    for (int i0 = 0; i0 < nbp; i0 += PD) {
 #pragma unroll
-    for (int k = 0; k < PD; ++k) {
-      step(pf[k]);
-      if (p + k < total && alive) body();
+      for (int k = 0; k < PD; ++k) {
+        step(pf[k]);
+        if (i0 + k < nbt) wbody(i0 + k);
+        else asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+      }
     }
+    end_iteration(it);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
 }
@@ -5766,18 +5989,20 @@ struct WaLaunch {
   int64_t G, n_tiles;
   size_t lds;
 };
-// workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2; 2: two waves per SIMD to hide the
-// fp64 and LDS latencies of the W-step, at 256 registers per lane)
+// workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2, default 2: two waves per SIMD hide the
+// fp64 and LDS latencies of the W-step, at 256 registers per lane and PD = 2; measured on one box,
+// cfg5: 146.6 us per iteration at 1, 123.1 us at 2, profiles/r02/session5/als_iter)
 static int wa_occ() {
-  static const int v = getenv("CNMF_ALS_OCC") && atoi(getenv("CNMF_ALS_OCC")) == 2 ? 2 : 1;
+  static const int v = getenv("CNMF_ALS_OCC") && atoi(getenv("CNMF_ALS_OCC")) == 1 ? 1 : 2;
   return v;
 }
+static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
 static PassFn wa_fn() {
   return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1>)
-                       : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 2>);
+                       : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
 }
 static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out) {
-  constexpr int PD = 3;
+  const int PD = wa_pd();
   if (x_dtype != CNMF_F32 || F != wt::F || k != wa::K || n_rows <= 0 || n_rows % wa::TSW != 0) return false;
   if (getenv("CNMF_ALS_PERSIST") && atoi(getenv("CNMF_ALS_PERSIST")) == 0) return false;
   const int64_t n_tiles = n_rows / wa::TSW;

@@ -16,6 +16,7 @@ SK:<line> = sklearn/decomposition/_nmf.py (1.7.2).
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 
 import torch
@@ -484,8 +485,10 @@ class ALSPlan(MUPlan):
 
     def describe(self) -> str:
         if self.persistent:
-            return ("als_iter_wt_kernel<PD=3>: wave tiles of 16 samples, one 4-wave workgroup per CU, "
-                    "in-launch reduction and H-step (every workgroup)")
+            occ2 = os.environ.get("CNMF_ALS_OCC", "2") != "1"
+            return (f"als_iter_wt_kernel<PD={2 if occ2 else 3}, {2 if occ2 else 1} workgroups per CU>: wave "
+                    "tiles of 16 samples, 4-wave workgroups, in-launch reduction and H-step (one-wave "
+                    "block-cyclic-reduction NNLS solves, every workgroup)")
         return "ALS W-step pass + cnmf_reduce_partials + als_basis_kernel per iteration"
 
     def tune(self, *args, **kwargs) -> dict:

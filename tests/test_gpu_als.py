@@ -68,7 +68,7 @@ def test_w_step_matches_scipy_nnls(F, k, delta):
     np.testing.assert_allclose(AB[:, F:], Wg.T @ Wg, rtol=2e-6)
 
 
-@pytest.mark.parametrize("F", [17, 81, 300])
+@pytest.mark.parametrize("F", [17, 81, 128, 129, 300])  # <= 128: one-wave PCR form; above: workgroup LDLᵀ
 @pytest.mark.parametrize("lam", [0.0, 0.5, 20.0])
 def test_h_step_matches_scipy_nnls(F, lam):
     import torch

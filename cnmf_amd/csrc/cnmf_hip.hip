@@ -907,22 +907,27 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
   for (int r = 0; r < 4; ++r) bacc64[r] = 0.0;
 
   u32x4 pf[PFN];
+  STAMP_DECL
   int64_t tile = blockIdx.x;
   if (tile < n_tiles) prefetch_tile<PFN>(pf, tile_geom(X, W, tile, n_rows, F, k), t);
 
   for (; tile < n_tiles; tile += gridDim.x) {
+    STAMP(0);
     const TileGeom gm = tile_geom(X, W, tile, n_rows, F, k);
     const int ns = gm.ns;
     stage_tile<bf16_t, float, PFN>(smem, L.w, gm, pf, t, F);
+    STAMP(1);  // 1: wait for this tile's loads + LDS writes
     if (ns < TS) {  // ragged tile: rows >= ns must hold finite values for the MFMA reads
       uint16_t* sx = reinterpret_cast<uint16_t*>(smem + L.x);
       for (int e = ns * F + 4 + t; e < TS * F; e += NT) sx[e] = 0;
     }
     __syncthreads();
+    STAMP(2);  // 2: staging barrier
     {
       const int64_t nt = tile + gridDim.x;
       if (nt < n_tiles) prefetch_tile<PFN>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
     }
+    STAMP(3);  // 3: prefetch issue
 
     // ---- phase 1: num for samples 16·wave + (4g + r), component li
     f32x4 num;
@@ -949,6 +954,7 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
       }
     }
 
+    STAMP(4);  // 4: phase 1
     // ---- phase 2: MU update of w[s][n], s = 16·wave + 4g + r, n = li (SK:526-631).
     // den = W·HHᵀ on v_mfma_f64_16x16x4_f64 (exact fp64 products and sums; f64 C/D layout: row =
     // g + 4·reg): its A-operand row ρ carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is sample 4g + r,
@@ -980,6 +986,7 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
       }
     }
     __syncthreads();  // every wave's W'ᵀ rows feed every wave's phase 3
+    STAMP(5);  // 5: phase 2 + barrier
 
     // ---- phase 3: acc[m = 4g + r][f = 16·nb + li] += Σ_s w'[s][m]·x[s][f]; B on f32 MFMA
     if (do_acc) {
@@ -1039,7 +1046,9 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
       for (int r = 0; r < 4; ++r) bacc64[r] += (double)bacc[r];
     }
     __syncthreads();  // LDS tiles are rewritten by the next iteration
+    STAMP(6);  // 6: phase 3 + end barrier
   }
+  STAMP_FLUSH;
 
   // ---- per-workgroup partial row [k][F + k]: A from each wave's own blocks, B summed over waves
   if (do_acc) {

@@ -166,10 +166,10 @@ __device__ __forceinline__ TileGeom tile_geom(const TX* X, const TC* W, int64_t 
 // re-read chunk 0 (an L1/L2 hit) instead of sitting in a divergent `if` — guarded loads made hipcc
 // put an `s_waitcnt vmcnt(0)` in front of every load, serialising the prefetch (and waiting on the
 // previous tile's W stores).
-template <int N>
+template <int N, int I0 = 0, int I1 = N>
 __device__ __forceinline__ void prefetch_tile(u32x4 (&pf)[N], const TileGeom& g, int t) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
+  for (int i = I0; i < I1; ++i) {
     const int c = t + NT * i;
     const size_t off = c < g.nxf ? 16 * (size_t)c : (c < g.nch ? 16 * (size_t)(c - g.nxf) : 0);
     const unsigned char* base = (c < g.nxf || c >= g.nch) ? g.xsrc : g.wsrc;
@@ -923,10 +923,12 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
     }
     __syncthreads();
     STAMP(2);  // 2: staging barrier
-    {
-      const int64_t nt = tile + gridDim.x;
-      if (nt < n_tiles) prefetch_tile<PFN>(pf, tile_geom(X, W, nt, n_rows, F, k), t);
-    }
+    // the next tile's loads in two halves (here and after phase 1): issuing all eleven 16-byte
+    // loads per thread at once stalled the issue on vector-memory back-pressure
+    // (profiles/r02/session5/diag2/stamps_bf16.log)
+    const int64_t nxt = tile + gridDim.x;
+    const TileGeom gnx = tile_geom(X, W, nxt < n_tiles ? nxt : tile, n_rows, F, k);
+    if (nxt < n_tiles) prefetch_tile<PFN, 0, PFN / 2>(pf, gnx, t);
     STAMP(3);  // 3: prefetch issue
 
     // ---- phase 1: num for samples 16·wave + (4g + r), component li
@@ -954,6 +956,7 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
       }
     }
 
+    if (nxt < n_tiles) prefetch_tile<PFN, PFN / 2, PFN>(pf, gnx, t);
     STAMP(4);  // 4: phase 1
     // ---- phase 2: MU update of w[s][n], s = 16·wave + 4g + r, n = li (SK:526-631).
     // den = W·HHᵀ on v_mfma_f64_16x16x4_f64 (exact fp64 products and sums; f64 C/D layout: row =

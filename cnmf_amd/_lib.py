@@ -76,6 +76,8 @@ _SIGS = {
     "cnmf_als_persistent": (_i32, [_i64, _i32, _i32, _i32]),
     "cnmf_als_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64,
                                    _i32, _i32, _f64, _f64, _vp, _i32, _vp]),
+    "cnmf_als_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                         _i64, _i32, _i32, _f64, _f64, _vp, _vp, _i32, _vp]),
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                   _i32, _f64, _f64, _f64, _f64, _i32, _vp]),

@@ -5097,6 +5097,7 @@ struct AlsPersistArgs {
   int n_groups;
   double delta2;     // sum_to_one²
   double lam;        // smoothness
+  uint64_t* xctl;    // MULTI: the cross-rank exchange control block (mu_iter_wt_kernel's protocol)
 };
 
 // Hᵀ (fp64, the lanes' feature blocks), HHᵀ (fp64; 16 threads per entry, fixed xor tree) and the
@@ -5146,7 +5147,7 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
   wa_derive(smem, t, delta2);
 }
 
-template <int PD, int OCC>
+template <int PD, int OCC, bool MULTI = false>
 __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
@@ -5360,6 +5361,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AB, sAB, err, it, t);  // + the other ranks' AB
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0 && !last_it)
@@ -5381,6 +5383,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
@@ -6009,11 +6013,14 @@ static int wa_occ() {
   return v;
 }
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
-static PassFn wa_fn() {
+static PassFn wa_fn(bool multi = false) {
+  if (multi)
+    return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true>)
+                         : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>);
   return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1>)
                        : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
 }
-static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out) {
+static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false) {
   const int PD = wa_pd();
   if (x_dtype != CNMF_F32 || F != wt::F || k != wa::K || n_rows <= 0 || n_rows % wa::TSW != 0) return false;
   if (getenv("CNMF_ALS_PERSIST") && atoi(getenv("CNMF_ALS_PERSIST")) == 0) return false;
@@ -6023,7 +6030,7 @@ static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out) {
   if (G < 1) return false;
   const size_t lds = (size_t)wa::L_HS + als_lds_bytes(F, k);
   if (lds > kMaxLds) return false;
-  if (max_resident(wa_fn(), lds) < G) return false;
+  if (max_resident(wa_fn(multi), lds) < G) return false;
   *out = WaLaunch{G, n_tiles, lds};
   return true;
 }
@@ -6033,13 +6040,14 @@ int cnmf_als_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   return wa_plan(n_rows, x_dtype, n_features, k, &L) ? 1 : 0;
 }
 
-int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
-                        double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
-                        double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
-                        void* const* events, int n_events, void* stream) {
+static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                          double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                          double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
+                          uint64_t* xctl, void* const* events, int n_events, void* stream) {
   if (n_iter <= 0) return CNMF_OK;
   WaLaunch L;
-  if (!wa_plan(n_rows, x_dtype, n_features, k, &L))
+  const bool multi = xctl != nullptr;
+  if (!wa_plan(n_rows, x_dtype, n_features, k, &L, multi))
     return set_err(CNMF_ERR_UNSUPPORTED, "the persistent constrained ALS serves fp32 F=81 k=4 with rows a multiple "
                    "of 16 (n_rows=%lld F=%d k=%d)", (long long)n_rows, n_features, k);
   if (!X || !W || !H64 || !Ht || !HHt || !table || !partials || !stage || !counter || !AB)
@@ -6066,11 +6074,30 @@ int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double*
   pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
   pa.delta2 = sum_to_one * sum_to_one;
   pa.lam = smoothness;
+  pa.xctl = xctl;
   void* args[] = {&pa};
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
-  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn()), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));
+  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn(multi)), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;
+}
+
+int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                        double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                        double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
+                        void* const* events, int n_events, void* stream) {
+  return als_iterations(n_iter, X, x_dtype, W, H64, Ht, HHt, table, partials, n_parts, stage, counter, AB, n_rows,
+                        n_features, k, sum_to_one, smoothness, nullptr, events, n_events, stream);
+}
+
+int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
+                              double* HHt, double* table, double* partials, int64_t n_parts, double* stage,
+                              uint32_t* counter, double* AB, int64_t n_rows, int n_features, int k,
+                              double sum_to_one, double smoothness, uint64_t* xctl, void* const* events,
+                              int n_events, void* stream) {
+  if (!xctl && n_iter > 0) return set_err(CNMF_ERR_ARG, "null exchange control block");
+  return als_iterations(n_iter, X, x_dtype, W, H64, Ht, HHt, table, partials, n_parts, stage, counter, AB, n_rows,
+                        n_features, k, sum_to_one, smoothness, xctl, events, n_events, stream);
 }
 
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,

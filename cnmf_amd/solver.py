@@ -500,13 +500,17 @@ class ALSPlan(MUPlan):
         if n_iter <= 0:
             return
         if self.persistent and update_H:
-            with torch.cuda.device(self.device):
-                check(self.lib.cnmf_als_iterations(
-                    n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
+            args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.table), _ptr(self.partials), self.n_parts,
                     _ptr(self.stage), _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
-                    self.delta, self.lam, *_event_array(pass_events), self._stream()),
-                    "cnmf_als_iterations")
+                    self.delta, self.lam)
+            with torch.cuda.device(self.device):
+                if self.exchange:  # several GPUs: the AB all-reduce inside the launch (enable_exchange)
+                    check(self.lib.cnmf_als_iterations_multi(*args, _ptr(self.xctl), *_event_array(pass_events),
+                                                             self._stream()), "cnmf_als_iterations_multi")
+                else:
+                    check(self.lib.cnmf_als_iterations(*args, *_event_array(pass_events), self._stream()),
+                          "cnmf_als_iterations")
             return
         ev = list(pass_events) if pass_events is not None else None
         stream = torch.cuda.current_stream(self.device) if ev is not None else None

@@ -224,6 +224,15 @@ int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double*
                         double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
                         double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
                         void* const* events, int n_events, void* stream);
+/* The same on several GPUs, one launch per rank: each rank's reduced [WᵀX | WᵀW] is summed with the
+ * other ranks' inside the launch (the in-launch exchange of cnmf_mu_iterations_multi: xctl from
+ * cnmf_xctl_init over buffers from cnmf_xbuf_alloc / cnmf_xbuf_open), so every rank applies the
+ * same H-step.  Every rank must issue the same sequence of launches. */
+int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
+                              double* HHt, double* table, double* partials, int64_t n_parts, double* stage,
+                              uint32_t* counter, double* AB, int64_t n_rows, int n_features, int k,
+                              double sum_to_one, double smoothness, uint64_t* xctl, void* const* events,
+                              int n_events, void* stream);
 
 /* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
  * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */

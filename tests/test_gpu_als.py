@@ -189,3 +189,102 @@ def test_persistent_als_tol_stop_matches_oracle():
                                  max_iter=200, tol=1e-3, sum_to_one=1.0, smoothness=0.1)
     assert n == nr
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5
+
+
+# ---- multi-GPU: the persistent ALS with the [WᵀX | WᵀW] all-reduce inside the launch
+
+def _port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _als_plan_group(X, W0, H0, delta, lam, group):
+    import torch
+    from cnmf_amd.solver import ALSPlan
+    plan = ALSPlan(torch.from_numpy(X).cuda(), H0.shape[0], sum_to_one=delta, smoothness=lam, group=group)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    return plan
+
+
+def test_persistent_als_self_exchange_is_bit_identical():
+    """One rank exchanging with itself (world-1 group): the multi-GPU launch sums its AB once, so the
+    factors are bit-identical to the single-GPU launch, across launches (the generation carries)."""
+    import torch
+    import torch.distributed as dist
+    X, W0, H0 = _mixtures(40000, 81, 4, seed=7)
+    ref = _plan(X, W0, H0, 1.0, 0.5)
+    assert ref.persistent
+    ref.iterate(12)
+    ref.check_sync_error()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        plan = _als_plan_group(X, W0, H0, 1.0, 0.5, dist.group.WORLD)
+        plan.enable_exchange()
+        assert plan.exchange and plan.persistent
+        plan.iterate(5)
+        plan.iterate(7)
+        plan.check_sync_error()
+        torch.cuda.synchronize()
+        assert int(plan.xctl[3].item()) == 12  # the device-side generation base
+        assert torch.equal(plan.W, ref.W) and torch.equal(plan.H64, ref.H64)
+        assert torch.equal(plan.table, ref.table)
+        assert plan.counters_at_rest()
+        plan.release()
+    finally:
+        dist.destroy_process_group()
+
+
+def _als_rank_main(rank, world, port, N, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        X, W0, H0 = _data(N, 81, 4, seed=21)
+        lo, hi = rank * N // world, (rank + 1) * N // world
+        plan = _als_plan_group(X[lo:hi].copy(), W0[lo:hi].copy(), H0, 1.0, 0.5, dist.group.WORLD)
+        plan.enable_exchange()
+        plan.iterate(9)
+        plan.iterate(11)
+        plan.check_sync_error()
+        q.put((rank, plan.W.cpu().numpy(), plan.H64.cpu().numpy(), None))
+        dist.barrier()
+        plan.release()
+        dist.destroy_process_group()
+    except Exception as ex:  # reported to the parent
+        q.put((rank, None, None, f"{type(ex).__name__}: {ex}"))
+
+
+@pytest.mark.timeout(600)
+def test_persistent_als_two_ranks_one_gpu_exchange():
+    """Two processes on one GPU, each with half the rows, exchanging AB through IPC-mapped buffers
+    inside the persistent ALS launch: the same H on both ranks, the fp64 oracle at 1e-5."""
+    import multiprocessing as mp
+    world, N = 2, 2 * 16 * 600  # 600 16-sample tiles per rank
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_als_rank_main, args=(r, world, port, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, W, H, err = q.get(timeout=400)
+            out[r] = (W, H, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [v[2] for v in out.values() if v[2]]
+    assert not errs, errs
+    np.testing.assert_array_equal(out[0][1], out[1][1])  # rank-ordered sums: the same H everywhere
+    W = np.concatenate([out[0][0], out[1][0]])
+    X, W0, H0 = _data(N, 81, 4, seed=21)
+    Wr, Hr, _ = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                max_iter=20, tol=0.0, sum_to_one=1.0, smoothness=0.5)
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(out[0][1], Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(out[0][1], Hr))

@@ -90,14 +90,14 @@ def test_self_exchange_is_bit_identical(layout):
         dist.destroy_process_group()
 
 
-def _rank_main(rank, world, port, N, q):
+def _rank_main(rank, world, port, N, q, k=4):
     try:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                 world_size=world)
-        X, W0, H0 = _data(N, 7)
+        X, W0, H0 = _data(N, 7, k=k)
         lo, hi = rank * N // world, (rank + 1) * N // world
         plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0, group=dist.group.WORLD)
         plan.enable_exchange()
@@ -114,14 +114,17 @@ def _rank_main(rank, world, port, N, q):
 
 
 @pytest.mark.timeout(600)
-def test_two_ranks_one_gpu_exchange():
+@pytest.mark.parametrize("k", [4, 8])
+def test_two_ranks_one_gpu_exchange(k):
+    """Two processes on one GPU exchanging through IPC-mapped buffers inside the persistent launch
+    (k = 8: cfg3's shape, the wave-tile kernel's xchg_allreduce_n over 712 accumulators)."""
     import torch
-    world, N = 2, 2 * 64 * 128  # 128 tiles per rank -> a 32-workgroup persistent grid each
+    world, N = 2, 2 * 64 * 128  # 128 64-row tiles per rank
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, N, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, N, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -140,7 +143,7 @@ def test_two_ranks_one_gpu_exchange():
     H0_, H1_ = out[0][1], out[1][1]
     np.testing.assert_array_equal(H0_, H1_)  # rank-ordered sums: the same H everywhere
     W = np.concatenate([out[0][0], out[1][0]])
-    X, W0, H0 = _data(N, 7)
+    X, W0, H0 = _data(N, 7, k=k)
     ref = _plan(X, W0, H0)
     ref.iterate(30)
     ref.check_sync_error()

@@ -173,8 +173,9 @@ def validate_exchange(plan, W0, H0d, n=20):
     # the two paths may run different kernels (the exchange: the persistent launch; RCCL: one
     # shard-step launch per iteration), whose fp32 partial sums are grouped differently: agreement
     # to that noise, the parity bar's hundredth
-    # (the constrained ALS: its exact FCLS amplifies that noise by cond(Q_PP): the parity bar itself)
-    bar = 1e-5 if getattr(plan, "lam", None) is not None else 1e-6
+    # (the constrained ALS and the weighted MU: their per-iteration kernels sum differently again and
+    # the ALS's exact FCLS amplifies that noise by cond(Q_PP): the parity bar itself)
+    bar = 1e-6 if type(plan).__name__ == "MUPlan" else 1e-5
     bad = fail or (not same) or not (dH < bar and dW < bar)
     st = torch.tensor([1.0 if bad else 0.0, dH, dW], dtype=torch.float64, device=dev)
     dist.all_reduce(st, op=dist.ReduceOp.MAX)
@@ -258,7 +259,7 @@ def main():
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     exchange = None
-    if args.solver in ("mu", "als") and not args.weighted and dist_path and args.exchange == "auto" and plan.persistent_shape:
+    if dist_path and args.exchange == "auto" and plan.persistent_shape:
         exchange = validate_exchange(plan, W0, H0d)
         print(f"[rank {rank}] in-launch exchange: {exchange}", file=sys.stderr, flush=True)
     elif args.dist and args.solver == "mu" and not args.weighted:

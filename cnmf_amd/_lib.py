@@ -67,6 +67,8 @@ _SIGS = {
     "cnmf_wmu_persistent": (_i32, [_i64, _i32, _i32]),
     "cnmf_wmu_iterations": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32, _i32,
                                    _vp, _i32, _vp]),
+    "cnmf_wmu_iterations_multi": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
+                                         _i32, _vp, _vp, _i32, _vp]),
     "cnmf_counter_err_word": (_i32, []),
     "cnmf_mu_persistent": (_i32, [_i64, _i32, _i32, _i32]),
     "cnmf_als_table_doubles": (_i32, []),

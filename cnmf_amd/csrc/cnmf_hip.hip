@@ -4687,6 +4687,7 @@ struct WmuPersistArgs {
   int64_t n_tiles;
   int n_iter;
   int n_groups;
+  uint64_t* xctl;    // MULTI: the cross-rank exchange control block (mu_iter_wt_kernel's protocol)
 };
 
 // Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) from the fp64 H in LDS
@@ -4734,7 +4735,7 @@ __device__ __forceinline__ void wait_set12(u32x4 (&pf)[12]) {
 }
 }  // namespace cnmf::wt
 
-template <int PD>
+template <int PD, bool MULTI = false>
 __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
@@ -4981,6 +4982,7 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AD
         sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAD, a.AD, t);
+        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AD, sAD, err, it, t);  // + the other ranks' [A|D]
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0 && !last_it)
@@ -5004,6 +5006,8 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
@@ -5984,7 +5988,7 @@ struct WwLaunch {
   int64_t G, n_tiles;
   size_t lds;
 };
-static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out) {
+static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out, bool multi = false) {
   constexpr int PD = 2;
   if (F != wt::F || k != ww::K || n_rows <= 0 || n_rows % ww::TSW != 0) return false;
   if (getenv("CNMF_WMU_PERSIST") && atoi(getenv("CNMF_WMU_PERSIST")) == 0) return false;
@@ -5995,7 +5999,9 @@ static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out) {
   const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
   const size_t lds = (size_t)ww::L_WRES + (size_t)wt::NWV * nbt_max * wt::Geo<4>::WBW;
   if (lds > kMaxLds) return false;  // W does not fit in LDS: the per-iteration pass serves it
-  if (max_resident(reinterpret_cast<PassFn>(&wmu_iter_wt_kernel<PD>), lds) < G) return false;
+  const PassFn fn = multi ? reinterpret_cast<PassFn>(&wmu_iter_wt_kernel<PD, true>)
+                          : reinterpret_cast<PassFn>(&wmu_iter_wt_kernel<PD>);
+  if (max_resident(fn, lds) < G) return false;
   *out = WwLaunch{G, n_tiles, lds};
   return true;
 }
@@ -6543,12 +6549,13 @@ int cnmf_wmu_persistent(int64_t n_rows, int n_features, int k) {
   return ww_plan(n_rows, n_features, k, &L) ? 1 : 0;
 }
 
-int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
-                        int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
-                        int n_features, int k, void* const* events, int n_events, void* stream) {
+static int wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                          int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                          int n_features, int k, uint64_t* xctl, void* const* events, int n_events, void* stream) {
   if (n_iter <= 0) return CNMF_OK;
   WwLaunch L;
-  if (!ww_plan(n_rows, n_features, k, &L))
+  const bool multi = xctl != nullptr;
+  if (!ww_plan(n_rows, n_features, k, &L, multi))
     return set_err(CNMF_ERR_UNSUPPORTED, "the persistent weighted MU serves fp32 F=81 k=4 with rows a multiple "
                    "of 16 whose W fits in LDS (n_rows=%lld F=%d k=%d)", (long long)n_rows, n_features, k);
   if (!X || !M || !W || !H64 || !partials || !stage || !counter || !AD)
@@ -6571,12 +6578,30 @@ int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, do
   pa.n_tiles = L.n_tiles;
   pa.n_iter = n_iter;
   pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  pa.xctl = xctl;
   void* args[] = {&pa};
+  const void* fn = multi ? reinterpret_cast<const void*>(&wmu_iter_wt_kernel<2, true>)
+                         : reinterpret_cast<const void*>(&wmu_iter_wt_kernel<2>);
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
-  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(&wmu_iter_wt_kernel<2>), dim3((unsigned)L.G), dim3(NT),
-                            args, L.lds, hs));
+  HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;
+}
+
+int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                        int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                        int n_features, int k, void* const* events, int n_events, void* stream) {
+  return wmu_iterations(n_iter, X, M, W, H64, partials, n_parts, stage, counter, AD, n_rows, n_features, k,
+                        nullptr, events, n_events, stream);
+}
+
+int cnmf_wmu_iterations_multi(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                              int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                              int n_features, int k, uint64_t* xctl, void* const* events, int n_events,
+                              void* stream) {
+  if (!xctl && n_iter > 0) return set_err(CNMF_ERR_ARG, "null exchange control block");
+  return wmu_iterations(n_iter, X, M, W, H64, partials, n_parts, stage, counter, AD, n_rows, n_features, k, xctl,
+                        events, n_events, stream);
 }
 
 int cnmf_wmu_basis_update(const double* AD, double* H64, int n_features, int k, void* stream) {

@@ -623,12 +623,16 @@ class WeightedMUPlan:
         if n_iter <= 0:
             return
         if self.persistent and update_H:
+            args = (n_iter, _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64), _ptr(self.partials),
+                    self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AD), self.n_rows, self.F,
+                    self.k)
             with torch.cuda.device(self.device):
-                check(self.lib.cnmf_wmu_iterations(
-                    n_iter, _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64),
-                    _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
-                    _ptr(self.AD), self.n_rows, self.F, self.k, *_event_array(pass_events),
-                    self._stream()), "cnmf_wmu_iterations")
+                if self.exchange:  # several GPUs: the [A | D] all-reduce inside the launch
+                    check(self.lib.cnmf_wmu_iterations_multi(*args, _ptr(self.xctl), *_event_array(pass_events),
+                                                             self._stream()), "cnmf_wmu_iterations_multi")
+                else:
+                    check(self.lib.cnmf_wmu_iterations(*args, *_event_array(pass_events), self._stream()),
+                          "cnmf_wmu_iterations")
             return
         ev = list(pass_events) if pass_events is not None else None
         stream = torch.cuda.current_stream(self.device) if ev is not None else None
@@ -654,8 +658,19 @@ class WeightedMUPlan:
         """Raise if the persistent launch gave up waiting for a workgroup (results invalid)."""
         if self.persistent_shape and int(self.counter[self.err_word].item()) != 0:
             self.counter.zero_()
+            if self.exchange:
+                self.disable_exchange()  # the buffer set's flags are poisoned: never reuse it
+                raise _lib.HipLibraryError("multi-GPU persistent weighted MU launch failed; the plan is back "
+                                           "on the RCCL path and the results of that launch are invalid")
             raise _lib.HipLibraryError("persistent weighted MU launch timed out waiting for a workgroup "
                                        "(grid not co-resident?); results of that launch are invalid")
+
+    # the in-launch cross-rank exchange (MUPlan's: IPC-shared buffers, cnmf_xctl_init), for the
+    # persistent weighted launch; collective over the plan's group
+    enable_exchange = MUPlan.enable_exchange
+    disable_exchange = MUPlan.disable_exchange
+    release = MUPlan.release
+    _pci_bus_id = MUPlan._pci_bus_id
 
     def frobenius_error(self) -> float:
         """sqrt(Σ m·(x − w·h)²) over all ranks; synchronises."""

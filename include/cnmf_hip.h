@@ -268,6 +268,12 @@ int cnmf_wmu_persistent(int64_t n_rows, int n_features, int k);
 int cnmf_wmu_iterations(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
                         int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
                         int n_features, int k, void* const* events, int n_events, void* stream);
+/* The same on several GPUs, one launch per rank, the reduced [A | D] summed over the ranks inside the
+ * launch (the exchange of cnmf_mu_iterations_multi; xctl from cnmf_xctl_init). */
+int cnmf_wmu_iterations_multi(int n_iter, const float* X, const float* M, float* W, double* H64, double* partials,
+                              int64_t n_parts, double* stage, uint32_t* counter, double* AD, int64_t n_rows,
+                              int n_features, int k, uint64_t* xctl, void* const* events, int n_events,
+                              void* stream);
 
 
 /* ---- GPU NNDSVD initialisation (sklearn _initialize_nmf SK:317-373 over

@@ -210,3 +210,107 @@ def test_persistent_full_size():
     torch.cuda.empty_cache()
     Wr, Hr, _ = _oracle_fit(X, M, W0, H0, 10)
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+# ---- multi-GPU: the persistent weighted MU with the [A | D] all-reduce inside the launch
+
+def _port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _plan_group(X, M, W0, H0, group):
+    import torch
+    from cnmf_amd.solver import WeightedMUPlan
+    plan = WeightedMUPlan(torch.from_numpy(X).cuda(), torch.from_numpy(M).cuda(), W0.shape[1], group=group)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    return plan
+
+
+def _wdata(n, seed):
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(n, 81, seed=seed, dtype=np.float32)
+    M = _weights(X, seed + 1)
+    W0, H0 = random_init(X, 4, 42)
+    return X, M, W0, H0
+
+
+def test_persistent_self_exchange_is_bit_identical():
+    """One rank exchanging with itself: bit-identical to the single-GPU launch, across launches."""
+    import torch
+    import torch.distributed as dist
+    X, M, W0, H0 = _wdata(64 * 700, 3)
+    ref = _plan(X, M, W0, H0)
+    assert ref.persistent
+    ref.iterate(15)
+    ref.check_sync_error()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
+    try:
+        plan = _plan_group(X, M, W0, H0, dist.group.WORLD)
+        plan.enable_exchange()
+        assert plan.exchange and plan.persistent
+        plan.iterate(6)
+        plan.iterate(9)
+        plan.check_sync_error()
+        torch.cuda.synchronize()
+        assert int(plan.xctl[3].item()) == 15
+        assert torch.equal(plan.W, ref.W) and torch.equal(plan.H64, ref.H64)
+        plan.release()
+    finally:
+        dist.destroy_process_group()
+
+
+def _wmu_rank_main(rank, world, port, N, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        X, M, W0, H0 = _wdata(N, 5)
+        lo, hi = rank * N // world, (rank + 1) * N // world
+        plan = _plan_group(X[lo:hi].copy(), M[lo:hi].copy(), W0[lo:hi].copy(), H0, dist.group.WORLD)
+        plan.enable_exchange()
+        plan.iterate(11)
+        plan.iterate(14)
+        plan.check_sync_error()
+        q.put((rank, plan.W.cpu().numpy(), plan.H64.cpu().numpy(), None))
+        dist.barrier()
+        plan.release()
+        dist.destroy_process_group()
+    except Exception as ex:  # reported to the parent
+        q.put((rank, None, None, f"{type(ex).__name__}: {ex}"))
+
+
+@pytest.mark.timeout(600)
+def test_persistent_two_ranks_one_gpu_exchange():
+    """Two processes on one GPU, half the rows each, exchanging [A | D] through IPC-mapped buffers
+    inside the persistent weighted launch: the same H on both ranks, the fp64 oracle at 1e-5."""
+    import multiprocessing as mp
+    world, N = 2, 2 * 16 * 700
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_wmu_rank_main, args=(r, world, port, N, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, W, H, err = q.get(timeout=400)
+            out[r] = (W, H, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [v[2] for v in out.values() if v[2]]
+    assert not errs, errs
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    W = np.concatenate([out[0][0], out[1][0]])
+    X, M, W0, H0 = _wdata(N, 5)
+    Wr, Hr, _ = wmu_ref.wmu_fit(X.astype(np.float64), M.astype(np.float64), W0.astype(np.float64),
+                                H0.astype(np.float64), max_iter=25, tol=0)
+    assert rel_fro(W, Wr) <= TOL32 and rel_fro(out[0][1], Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(out[0][1], Hr))

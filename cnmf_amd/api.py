@@ -340,7 +340,7 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
     `sklearn.decomposition.non_negative_factorization` (SK:905-1131), except solver defaults to
-    (and must be) 'mu'.  `device` selects the HIP device (default: current).
+    'mu' and takes 'mu' or 'als' (no 'cd').  `device` selects the HIP device (default: current).
     `normalise` ('l1' | 'l2' | 'max' | None, default None = sklearn's output): after the fit, every
     row of H is scaled to unit norm and the scale folded into W's column (W·H unchanged;
     SURVEY.md §8 a6).

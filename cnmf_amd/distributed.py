@@ -19,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .solver import MUPlan, WeightedMUPlan, run_mu
+from .solver import ALSPlan, MUPlan, WeightedMUPlan, run_mu
 
 __all__ = ["shard_bounds", "factorise_sharded"]
 
@@ -41,7 +41,7 @@ def shard_bounds(n_rows: int, world: int, rank: int, align: int = 1):
 
 def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=0.0, l2_reg_W=0.0,
                       l1_reg_H=0.0, l2_reg_H=0.0, update_H=True, group=None, device=None,
-                      exchange=False, weights=None):
+                      exchange=False, weights=None, solver="mu", sum_to_one=0.0, smoothness=0.0):
     """MU on this rank's rows; returns (W_shard, H, n_iter) as device tensors.
 
     X_shard: (n_r, F) float32/float64/bfloat16 tensor (any device; moved to `device`, default the
@@ -56,7 +56,10 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
 
     weights: this rank's rows of the per-element weights (float32 X): the
     weighted / masked MU, whose 2kF accumulators [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))] are all-reduced the
-    same way (no regularisation, no exchange).
+    same way (no regularisation).
+    solver='als': the constrained ALS (sum_to_one, smoothness), its [WᵀX | WᵀW]
+    all-reduced before every H-step.  Both take exchange=True (fp32, F = 81, k = 4, rows a multiple
+    of 16): one persistent launch per rank with the all-reduce inside it.
     """
     if not (dist.is_available() and dist.is_initialized()):
         raise RuntimeError("factorise_sharded needs an initialised torch.distributed process group")
@@ -65,16 +68,20 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     X = torch.as_tensor(X_shard).to(dev).contiguous()
     H0 = torch.as_tensor(H0).to(dev, torch.float64).contiguous()
     dist.broadcast(H0, src=dist.get_global_rank(group, 0), group=group)
+    if solver not in ("mu", "als"):
+        raise ValueError(f"solver must be 'mu' or 'als', got {solver!r}")
+    if weights is not None or solver == "als":
+        if any((l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H)):
+            raise ValueError("the weighted MU and the constrained ALS take no l1/l2 regularisation")
+        if weights is not None and solver == "als":
+            raise ValueError("weights apply to solver='mu'")
     if weights is not None:
-        if any((l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H)) or exchange:
-            raise ValueError("the weighted MU takes no regularisation and no in-launch exchange")
         M = torch.as_tensor(weights).to(dev, torch.float32).contiguous()
         plan = WeightedMUPlan(X, M, H0.shape[0], group=group)
-        plan.set_W(torch.as_tensor(W_shard))
-        plan.set_H(H0)
-        n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H)
-        return plan.W, plan.H(), n_iter
-    plan = MUPlan(X, H0.shape[0], l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H, group=group)
+    elif solver == "als":
+        plan = ALSPlan(X, H0.shape[0], sum_to_one=sum_to_one, smoothness=smoothness, group=group)
+    else:
+        plan = MUPlan(X, H0.shape[0], l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H, group=group)
     plan.set_W(torch.as_tensor(W_shard))
     plan.set_H(H0)
     if exchange:

@@ -156,3 +156,50 @@ def test_two_process_weighted_shards_match_oracle():
                                  H0.astype(np.float64), max_iter=200, tol=1e-3)
     assert res[0][5] == nr
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def _sharded_als_worker(rank, world, port, X, W0, H0, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+        warnings.filterwarnings("error", message="in-launch exchange not used")  # no silent fallback
+        torch.cuda.set_device(0)
+        from cnmf_amd.distributed import factorise_sharded, shard_bounds
+        lo, hi = shard_bounds(X.shape[0], world, rank, align=64)
+        W, H, n = factorise_sharded(X[lo:hi], W0[lo:hi], H0, max_iter=25, tol=0.0, solver="als",
+                                    sum_to_one=1.0, smoothness=0.5, exchange=True)
+        q.put((rank, W.cpu().numpy(), H.cpu().numpy().astype(np.float64), n, None))
+    except Exception as ex:  # reported to the parent
+        q.put((rank, None, None, None, f"{type(ex).__name__}: {ex}"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_factorise_sharded_als_exchange_matches_oracle():
+    """The public sharded entry with solver='als' and exchange=True (the persistent ALS launch per rank
+    with the all-reduce inside it), two processes on one GPU, against the fp64 ALS oracle."""
+    import torch.multiprocessing as mp
+    from oracle import als_ref
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(64 * 300, 81, seed=6, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_als_worker, args=(r, 2, port, X, W0, H0, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs
+    assert np.array_equal(res[0][2], res[1][2])
+    W = np.concatenate([r[1] for r in res])
+    Wr, Hr, _ = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                max_iter=25, tol=0.0, sum_to_one=1.0, smoothness=0.5)
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(res[0][2], Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(res[0][2], Hr))

@@ -3744,7 +3744,7 @@ __device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, dou
 
 // The W-step's passive-set table from HHᵀ (stride KP): per mask (thread t < 16) the inverse of
 // Q_PP, Q = HHᵀ + δ²11ᵀ, by Gauss-Jordan with partial pivoting, scattered to 4x4, and the valid flag
-__device__ void als_table(const double* HHt, int KP, int k, double delta2, double* table, int t) {
+__device__ void als_table(const double* HHt, int KP, int k, double delta2, double* table, int t, int mstride = 16) {
   // Register-resident form (every index compile-time; the runtime-indexed compressed arrays went to
   // scratch): Gauss-Jordan on the full 4x4 [Q | I] with the rows / columns outside P held at the
   // identity.  The entries of P see exactly the compressed elimination's operations in the same
@@ -3806,9 +3806,9 @@ __device__ void als_table(const double* HHt, int KP, int k, double delta2, doubl
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const bool in = (mask >> r & 1) && (mask >> c & 1);
-        table[mask * 16 + r * 4 + c] = (valid && in) ? a[r][4 + c] : 0.0;
+        table[mask * mstride + r * 4 + c] = (valid && in) ? a[r][4 + c] : 0.0;
       }
-    table[256 + mask] = valid ? 1.0 : 0.0;
+    table[16 * mstride + mask] = valid ? 1.0 : 0.0;
   }
 }
 
@@ -5078,8 +5078,11 @@ constexpr int L_H = L_RED + wt::NWV * NL * NACC * 4;            // H fp64 [K][F]
 constexpr int L_AB = L_H + K * F * 8;                           // AB fp64 [K][V]
 constexpr int L_HT = L_AB + NOUT * 8;                           // Hᵀ fp64 [NL·NQ][K], rows >= F zero
 constexpr int L_HHT = L_HT + NL * NQ * K * 8;                   // HHᵀ fp64 [K][K]
-constexpr int L_TAB = L_HHT + K * K * 8;                        // passive-set table (ALS_TAB doubles)
-constexpr int L_FLAG = L_TAB + ALS_TAB * 8;                     // 4 ints
+// passive-set table, masks at a stride of TSTR doubles (18: the four masks a quad reads with one
+// ds_read_b128 land on disjoint banks; at 16 the masks e and e + 2 shared them), then 16 flags
+constexpr int TSTR = 18;
+constexpr int L_TAB = L_HHT + K * K * 8;
+constexpr int L_FLAG = L_TAB + (16 * TSTR + 16) * 8;            // 4 ints
 constexpr int L_HS = (L_FLAG + 16 + 15) / 16 * 16;              // als_hstep's arrays (als_lds_bytes)
 static_assert(L_RED % 16 == 0 && L_HT % 16 == 0 && L_HS % 16 == 0, "16-byte aligned LDS regions");
 static_assert(NOUT * 8 >= wt::NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
@@ -5125,7 +5128,7 @@ __device__ __forceinline__ void wa_derive(unsigned char* smem, int t, double del
   for (int o = TPE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if (part == 0) sHHt[en] = v;
   __syncthreads();
-  als_table(sHHt, K, K, delta2, reinterpret_cast<double*>(smem + L_TAB), t);
+  als_table(sHHt, K, K, delta2, reinterpret_cast<double*>(smem + L_TAB), t, TSTR);
   __syncthreads();
 }
 
@@ -5269,8 +5272,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int m = e + 4 * u;
-      const double* T = sTab + m * 16;
-      bool feas = sTab[256 + m] != 0.0;
+      const double* T = sTab + m * wa::TSTR;
+      bool feas = sTab[16 * wa::TSTR + m] != 0.0;
       double f = 0.0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -5297,7 +5300,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
     double wn64 = 0.0;
     {
-      const double* T = sTab + min(bestm, 15) * 16;
+      const double* T = sTab + min(bestm, 15) * wa::TSTR;
 #pragma unroll
       for (int q = 0; q < 4; ++q) wn64 = fma(T[e * 4 + q], cc[q], wn64);
     }
@@ -5382,7 +5385,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       for (int o = t; o < KK * wa::F; o += NT) a.H64[o] = sH[o];
       for (int o = t; o < wa::F * KK; o += NT) a.Ht[o] = reinterpret_cast<const double*>(smem + wa::L_HT)[o];
       if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + wa::L_HHT)[t];
-      for (int o = t; o < ALS_TAB; o += NT) a.table[o] = sTab[o];
+      for (int o = t; o < ALS_TAB; o += NT)  // the global table keeps the stride of 16
+        a.table[o] = o < 256 ? sTab[(o >> 4) * wa::TSTR + (o & 15)] : sTab[16 * wa::TSTR + (o - 256)];
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -6,7 +6,7 @@
 # own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-D=gpurun_out/final
+D=gpurun_out/final2
 mkdir -p $D/pmc
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 T="python -u -m pytest -x -v -p no:cacheprovider --timeout 180 --timeout-method thread"

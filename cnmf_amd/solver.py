@@ -49,6 +49,21 @@ def _event_array(events):
     return (ctypes.c_void_p * len(handles))(*handles), len(handles)
 
 
+def _prepared_call(fn, name, args, device):
+    """fn(*args) with the arguments converted once to their ctypes types (fn.argtypes); the call
+    itself runs on `device` (the current device when the plan's is already current)."""
+    cargs = tuple(None if a is None else t(a) if not isinstance(a, ctypes.Array) else a
+                  for a, t in zip(args, fn.argtypes))
+
+    def run():
+        if torch.cuda.current_device() != device.index:
+            with torch.cuda.device(device):
+                check(fn(*cargs), name)
+        else:
+            check(fn(*cargs), name)
+    return run
+
+
 class MUPlan:
     """Device state for the MU iterations on X (n_rows × F, samples-major, already on the GPU)."""
 
@@ -276,6 +291,27 @@ class MUPlan:
         """Every ticket, flag, pool and the error word back at zero."""
         return int(self.counter.cpu().numpy().astype("int64").sum()) == 0
 
+    def prepare(self, n_iter: int, pass_events=None):
+        """A zero-argument callable that runs `iterate(n_iter, pass_events=...)`: for the one-launch
+        paths the library call with its arguments marshalled up front (so a timed region holds the
+        launch itself, not the host's argument conversion), else a plain call of iterate."""
+        ev = _event_array(pass_events)
+        if getattr(self, "exchange", False):
+            fn, name = self.lib.cnmf_mu_iterations_multi, "cnmf_mu_iterations_multi"
+            args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                    _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AB),
+                    self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl),
+                    *ev, self._stream())
+        elif self.world == 1 and not self.shard_steps and self.persistent:
+            fn, name = self.lib.cnmf_mu_iterations, "cnmf_mu_iterations"
+            args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                    _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AB), None,
+                    self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H, *ev,
+                    self._stream())
+        else:
+            return lambda: self.iterate(n_iter, pass_events=pass_events)
+        return _prepared_call(fn, name, args, self.device)
+
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
         """n_iter MU iterations (SK:831-870) without host synchronisation.  pass_events: optional
         recorded-once torch.cuda.Event(enable_timing=True) list (single GPU only): 2 events around
@@ -494,6 +530,20 @@ class ALSPlan(MUPlan):
     def tune(self, *args, **kwargs) -> dict:
         return {}  # one layout
 
+    def prepare(self, n_iter: int, pass_events=None):
+        """As MUPlan.prepare, for the persistent ALS launch."""
+        if not self.persistent:
+            return lambda: self.iterate(n_iter, pass_events=pass_events)
+        args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self.table), _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
+                _ptr(self.AB), self.n_rows, self.F, self.k, self.delta, self.lam)
+        ev = _event_array(pass_events)
+        if self.exchange:
+            return _prepared_call(self.lib.cnmf_als_iterations_multi, "cnmf_als_iterations_multi",
+                                  args + (_ptr(self.xctl), *ev, self._stream()), self.device)
+        return _prepared_call(self.lib.cnmf_als_iterations, "cnmf_als_iterations",
+                              args + (*ev, self._stream()), self.device)
+
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
         """n_iter ALS iterations; pass_events: 2 events around the one launch when self.persistent,
         else 2·n_iter events around each W-step pass."""
@@ -616,6 +666,19 @@ class WeightedMUPlan:
             return ("wmu_iter_wt_kernel<k=4, W resident in LDS, PD=2>: wave tiles of 16 samples, X and the "
                     "weights prefetched together, one 4-wave workgroup per CU, in-launch reduction and H-step")
         return "wmu_pass_kernel + cnmf_reduce_partials + wmu_basis_kernel per iteration"
+
+    def prepare(self, n_iter: int, pass_events=None):
+        """As MUPlan.prepare, for the persistent weighted launch."""
+        if not self.persistent:
+            return lambda: self.iterate(n_iter, pass_events=pass_events)
+        args = (n_iter, _ptr(self.X), _ptr(self.M), _ptr(self.W), _ptr(self.H64), _ptr(self.partials),
+                self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AD), self.n_rows, self.F, self.k)
+        ev = _event_array(pass_events)
+        if self.exchange:
+            return _prepared_call(self.lib.cnmf_wmu_iterations_multi, "cnmf_wmu_iterations_multi",
+                                  args + (_ptr(self.xctl), *ev, self._stream()), self.device)
+        return _prepared_call(self.lib.cnmf_wmu_iterations, "cnmf_wmu_iterations",
+                              args + (*ev, self._stream()), self.device)
 
     def iterate(self, n_iter: int, update_H: bool = True, pass_events=None):
         """n_iter weighted MU iterations; pass_events: 2 events around the one launch when

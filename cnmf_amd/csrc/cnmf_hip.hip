@@ -1679,9 +1679,22 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
   double* red = sB + 256;             // [4 waves][64 lanes][4]
   double* sR = red + 4 * 64 * 4;      // [2][4]
   const bool upd = do_update && AB != nullptr;
-  for (int e = t; e < 16 * FP; e += RED_NT) {
-    const int j = e / FP, f = e - j * FP;
-    sH[e] = (j < k && f < F) ? H64[j * F + f] : 0.0;
+  // H into LDS with 8 loads per thread in flight (one load per trip of a runtime loop waited for each
+  // one in turn: 19 dependent global round trips at F = 300 were most of this kernel's 23 µs)
+  constexpr int UB = 8;
+  for (int e0 = t; e0 < 16 * FP; e0 += RED_NT * UB) {
+    double v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = e0 + u * RED_NT;
+      const int j = e / FP, f = e - j * FP;
+      const bool ok = e < 16 * FP && j < k && f < F;
+      const double x = H64[ok ? j * F + f : 0];
+      v[u] = ok ? x : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+      if (e0 + u * RED_NT < 16 * FP) sH[e0 + u * RED_NT] = v[u];
   }
   for (int e = t; e < 256; e += RED_NT) {
     const int j = e >> 4, m = e & 15;
@@ -1692,6 +1705,17 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
     constexpr int NBL = 8;  // F <= 512
     double hn[NBL][4];
     double bfr[4];
+    // this lane's numerators (WᵀX)[j][f], all loads in flight together
+    double nm[NBL][4];
+#pragma unroll
+    for (int i = 0; i < NBL; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = g + 4 * r, f = 16 * (wave + 4 * i) + li;
+        const bool ok = wave + 4 * i < NB && j < k && f < F;
+        const double x = AB[ok ? j * V + f : 0];
+        nm[i][r] = ok ? x : 0.0;
+      }
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) bfr[kk] = sB[li * 16 + 4 * kk + g];  // A[j = li][m = 4kk + g]
 #pragma unroll
@@ -1708,7 +1732,7 @@ __device__ void basis_update_mfma(const double* AB, double* H64, double* Ht, dou
         const int j = g + 4 * r;
         double h = sH[j * FP + f];
         if (j < k && f < F) {
-          const double num = AB[j * V + f];
+          const double num = nm[i][r];
           double d = den[r];
           if (l1 > 0.0) d += l1;                                // SK:702-703
           if (l2 > 0.0) d = d + l2 * h;                         // SK:704-705

@@ -52,6 +52,8 @@ def _event_array(events):
 def _prepared_call(fn, name, args, device):
     """fn(*args) with the arguments converted once to their ctypes types (fn.argtypes); the call
     itself runs on `device` (the current device when the plan's is already current)."""
+    if len(args) != len(fn.argtypes):
+        raise TypeError(f"{name}: {len(args)} arguments for {len(fn.argtypes)} parameters")
     cargs = tuple(None if a is None else t(a) if not isinstance(a, ctypes.Array) else a
                   for a, t in zip(args, fn.argtypes))
 

@@ -30,3 +30,25 @@ def test_error_paths_return_status():
     assert lib.cnmf_pass_blocks(100, 81, 4, 9) == -1   # unknown dtype
     with pytest.raises(_lib.HipLibraryError):
         _lib.check(-3, "probe")
+
+
+def test_prepared_calls_match_the_declared_signatures():
+    """plan.prepare marshals each one-launch entry's arguments once (solver._prepared_call); the
+    tuples it builds must match the ctypes signatures (checked here without a GPU call)."""
+    import ctypes
+    from cnmf_amd import _lib
+    from cnmf_amd.solver import _prepared_call
+    lib = _lib.load()
+    ev = ((ctypes.c_void_p * 2)(1, 2), 2)
+    calls = {
+        "cnmf_mu_iterations": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, None, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, *ev, 0),
+        "cnmf_mu_iterations_multi": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, 1, *ev, 0),
+        "cnmf_als_iterations": (20, 1, 0, 1, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 1.0, 0.5, *ev, 0),
+        "cnmf_als_iterations_multi": (20, 1, 0, 1, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 1.0, 0.5, 1, *ev, 0),
+        "cnmf_wmu_iterations": (20, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, *ev, 0),
+        "cnmf_wmu_iterations_multi": (20, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 1, *ev, 0),
+    }
+    import torch
+    for name, args in calls.items():
+        run = _prepared_call(getattr(lib, name), name, args, torch.device("cpu"))
+        assert callable(run)

@@ -77,21 +77,30 @@ def parse():
                         "tens of ms of work; the state is restored, the timed K steps are unchanged)")
     p.add_argument("--no-tune", action="store_true",
                    help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="torch.distributed backend at N > 1: nccl (= RCCL over xGMI, the default) or "
+                        "gloo (host-side collectives: lets two ranks share one GPU, as the N > 1 tests do)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
     return p.parse_args()
 
 
-def cpu_baseline(X, W0, H0, budget_s):
-    """Oracle fp32 MU iterations (SK:526-728 arithmetic via oracle/mu_ref.py) on the host cores."""
-    from oracle import mu_ref
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline line."""
     try:
-        from threadpoolctl import threadpool_info
-        info = threadpool_info()
-        threads = max((i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"), default=1)
-        blas = ",".join(sorted({f"{i.get('internal_api')}" for i in info if i.get("user_api") == "blas"}))
-    except Exception:  # pragma: no cover
-        threads, blas = os.cpu_count() or 1, "unknown"
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _time_oracle_mu(X, W0, H0, budget_s):
+    """Iterations per second of oracle/mu_ref.py's fp32 MU on the host: (it/s, iterations, seconds)."""
+    from oracle import mu_ref
     W, H = W0.copy(), H0.copy()
 
     def one():
@@ -101,18 +110,40 @@ def cpu_baseline(X, W0, H0, budget_s):
 
     t0 = time.perf_counter()
     one()
-    t1 = time.perf_counter()
-    per = max(t1 - t0, 1e-6)
+    per = max(time.perf_counter() - t0, 1e-6)
     n = int(max(2, min(200, budget_s / per)))
     t0 = time.perf_counter()
     for _ in range(n):
         one()
     el = time.perf_counter() - t0
-    return {"value": round(n / el, 4), "unit": "it/s", "cores": int(threads), "kind": "port",
+    return n / el, n, el
+
+
+def cpu_baseline(X, W0, H0, budget_s):
+    """Oracle fp32 MU iterations (SK:526-728 arithmetic via oracle/mu_ref.py) on the host cores:
+    with the BLAS threads the process has (os.cpu_count()-bounded, reported as `cores`) and with ONE
+    thread; the CPU model and BLAS vendor are named."""
+    try:
+        from threadpoolctl import threadpool_info, threadpool_limits
+        info = threadpool_info()
+        threads = max((i.get("num_threads", 1) for i in info if i.get("user_api") == "blas"), default=1)
+        blas = ",".join(sorted({f"{i.get('internal_api')}" for i in info if i.get("user_api") == "blas"}))
+    except Exception:  # pragma: no cover
+        threadpool_limits = None
+        threads, blas = os.cpu_count() or 1, "unknown"
+    value, n, el = _time_oracle_mu(X, W0, H0, budget_s)
+    one_thread = None
+    if threadpool_limits is not None:
+        with threadpool_limits(limits=1, user_api="blas"):
+            v1, n1, el1 = _time_oracle_mu(X, W0, H0, max(budget_s / 3.0, 1.0))
+        one_thread = {"value": round(v1, 4), "unit": "it/s", "cores": 1, "iterations": n1,
+                      "seconds": round(el1, 3)}
+    return {"value": round(value, 4), "unit": "it/s", "cores": int(threads), "kind": "port",
             "sample": f"{n} MU iterations (after 1 untimed) of oracle/mu_ref.py update_w+update_h, "
                       f"NumPy fp32 ({blas} BLAS, {threads} threads), on the same "
                       f"{X.shape[0]}x{X.shape[1]} k={W0.shape[1]} X as the GPU run",
-            "seconds": round(el, 3)}
+            "seconds": round(el, 3), "cpu_model": cpu_model(), "logical_cpus": os.cpu_count(),
+            "blas": blas, "one_thread": one_thread}
 
 
 def cpu_baseline_als(X, W0, H0, delta, lam, budget_s):
@@ -136,7 +167,7 @@ def cpu_baseline_als(X, W0, H0, delta, lam, budget_s):
     return {"value": round(1.0 / per_it_full, 6), "unit": "it/s", "cores": 1, "kind": "port",
             "sample": f"{it} ALS iterations of oracle/als_ref.py (scipy.optimize.nnls per sample, "
                       f"fp64, 1 thread) on the first {rows} of the {n} rows, scaled by {n}/{rows}",
-            "seconds": round(el, 3)}
+            "seconds": round(el, 3), "cpu_model": cpu_model(), "logical_cpus": os.cpu_count()}
 
 
 def validate_exchange(plan, W0, H0d, n=20):
@@ -191,6 +222,53 @@ def validate_exchange(plan, W0, H0d, n=20):
             f"H {float(st[1]):.2e} W {float(st[2]):.2e}")
 
 
+def any_rank(flag: bool, world: int, dev) -> bool:
+    """True on every rank when `flag` is True on any rank (a MAX all-reduce; identity at N = 1)."""
+    if world == 1:
+        return bool(flag)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64,
+                     device="cpu" if dist.get_backend() == "gloo" else dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]) != 0.0
+
+
+def rank0_says(flag: bool, world: int, dev) -> bool:
+    """Rank 0's `flag`, on every rank (a broadcast; identity at N = 1)."""
+    if world == 1:
+        return bool(flag)
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64,
+                     device="cpu" if dist.get_backend() == "gloo" else dev)
+    dist.broadcast(t, src=0)
+    return float(t[0]) != 0.0
+
+
+def clock_ramp(plan, seconds: float, world: int, dev, sync, trip: int = 100) -> tuple[float, int]:
+    """Untimed iterations on copies of W / H until `seconds` of wall time have passed on RANK 0's
+    clock: before every trip rank 0 broadcasts whether to go on, so every rank issues the same
+    launches (per-rank clocks could give one rank an extra 100-iteration trip, which on
+    the exchange path spins its launch into a timeout and on the RCCL path mis-pairs collectives).
+    The plan's state is restored afterwards.  Returns (seconds, trips)."""
+    W_keep = plan.W.clone()
+    H_keep = plan.H64.clone()
+    t_r = time.perf_counter()
+    trips = 0
+    while rank0_says(time.perf_counter() - t_r < seconds, world, dev):
+        plan.iterate(trip)
+        sync()
+        trips += 1
+    el = time.perf_counter() - t_r
+    plan.W.copy_(W_keep)
+    plan.H64.copy_(H_keep)
+    if hasattr(plan, "refresh_basis"):
+        plan.refresh_basis()
+    sync()
+    return el, trips
+
+
 def load_traffic(path, n_rows, F, k):
     """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py)."""
     try:
@@ -220,10 +298,15 @@ def main():
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
     dist_path = world > 1 or args.dist
+    # one GPU per rank; with --backend gloo several ranks may share a GPU (local % device count)
+    local_dev = local % max(torch.cuda.device_count(), 1)
     if dist_path:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(local_dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local_dev)
     torch.cuda.set_device(dev)
     group = dist.group.WORLD if dist_path else None
 
@@ -269,14 +352,13 @@ def main():
     plan.iterate(args.warmup)
     torch.cuda.synchronize()
     if getattr(plan, "exchange", False):  # a failed warmup launch falls back before anything is timed
-        fail = torch.zeros(1, dtype=torch.float64, device=dev)
+        fail = False
         try:
             plan.check_sync_error()
         except Exception as e:
-            fail[0] = 1.0
+            fail = True
             print(f"[rank {rank}] exchange warmup failed: {e}", file=sys.stderr, flush=True)
-        dist.all_reduce(fail, op=dist.ReduceOp.MAX)
-        if float(fail[0]) != 0.0:
+        if any_rank(fail, world, dev):
             plan.disable_exchange()
             exchange = "failed in warmup; RCCL path timed"
             plan.set_W(torch.from_numpy(W0))
@@ -287,30 +369,24 @@ def main():
     # clock ramp: after idle the chip runs its first tens of ms of work at lower clocks (r01/r02:
     # a 20-step timing after a 5-step warmup read 66 us per iteration against 57-58 us once warm);
     # run untimed iterations on copies of W / H until ramp_s of GPU time has passed
-    ramp_s = 0.0
+    ramp_s, ramp_trips = 0.0, 0
     if args.ramp_seconds > 0:
-        import torch as _t
-        W_keep = plan.W.clone()
-        H_keep = plan.H64.clone()
-        t_r = time.perf_counter()
-        while time.perf_counter() - t_r < args.ramp_seconds:
-            plan.iterate(100)
-            _t.cuda.synchronize()
-        ramp_s = time.perf_counter() - t_r
-        plan.W.copy_(W_keep)
-        plan.H64.copy_(H_keep)
-        if hasattr(plan, "refresh_basis"):
-            plan.refresh_basis()
-        _t.cuda.synchronize()
+        ramp_s, ramp_trips = clock_ramp(plan, args.ramp_seconds, world, dev, torch.cuda.synchronize)
         plan.check_sync_error()
 
     # the persistent launch has several layouts whose order can differ between boxes: time them on
-    # this box (warm clocks; copies of W / H, so the state is unchanged) and keep the fastest
+    # this box (warm clocks; copies of W / H, so the state is unchanged) and keep the fastest.  The
+    # choice is collective (MUPlan.tune max-reduces the times over the ranks): every rank launches
+    # the same layout
     tuned = {}
     if args.solver == "mu" and plan.persistent and not args.no_tune and not args.weighted:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
     layout = plan.describe() if plan.persistent else None
+    layouts = [getattr(plan, "layout", None)]
+    if world > 1:
+        layouts = [None] * world
+        dist.all_gather_object(layouts, getattr(plan, "layout", None))
     if layout and "floating" in layout:
         layout += " (80 % resident, 20 % drawn from a pool every iteration)"
 
@@ -339,14 +415,13 @@ def main():
 
     persistent, events, elapsed = timed()
     if getattr(plan, "exchange", False):  # a failed exchange launch: every rank re-times on RCCL
-        fail = torch.zeros(1, dtype=torch.float64, device=dev)
+        fail = False
         try:
             plan.check_sync_error()
         except Exception as e:
-            fail[0] = 1.0
+            fail = True
             print(f"[rank {rank}] exchange launch failed: {e}", file=sys.stderr, flush=True)
-        dist.all_reduce(fail, op=dist.ReduceOp.MAX)
-        if float(fail[0]) != 0.0:
+        if any_rank(fail, world, dev):
             plan.disable_exchange()
             exchange = "failed in the timed launch; RCCL path re-timed"
             plan.set_W(torch.from_numpy(W0))
@@ -364,10 +439,8 @@ def main():
                                       for i in range(K)])) / 1e3
     avg_pass_s = avg_launch_s
 
-    el_t = torch.tensor([elapsed, avg_pass_s], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    elapsed, avg_pass_s_max = float(el_t[0]), float(el_t[1])
+    from cnmf_amd.solver import agree_max
+    elapsed, avg_pass_s_max = agree_max([elapsed, avg_pass_s], dist.group.WORLD if world > 1 else None, dev)
 
     sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
     sw = 8 if args.dtype == "f64" else 4
@@ -399,8 +472,7 @@ def main():
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
     elif persistent:
-        variant = int(plan.lib.cnmf_get_persist_variant())
-        kbase = "mu_iter_wt_kernel" if variant == 4 else "mu_iter_sl_kernel"
+        kbase = "mu_iter_wt_kernel" if "mu_iter_wt_kernel" in (layout or "") else "mu_iter_sl_kernel"
         if world == 1:
             kname = (f"{kbase} (persistent: K iterations of pass + in-launch reduction + basis "
                      "update per launch)")
@@ -480,8 +552,10 @@ def main():
                                   + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
                    "exchange": exchange,
                    "persistent_layout": layout if plan.persistent else None,
+                   "layout_per_rank": layouts,
+                   "backend": (args.backend if dist_path else None),
                    "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None,
-                   "clock_ramp_s": round(ramp_s, 3)},
+                   "clock_ramp_s": round(ramp_s, 3), "clock_ramp_trips": ramp_trips},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

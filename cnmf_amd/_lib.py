@@ -54,13 +54,9 @@ _SIGS = {
     "cnmf_basis_update": (_i32, [_vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64, _i32, _vp, _vp]),
     "cnmf_reduce_update": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _f64, _f64,
                                   _vp, _vp]),
-    "cnmf_hbm_probe": (_i32, [_vp, _i64, _vp, _i32, _vp]),
     "cnmf_mu_iterations": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
-                                  _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _vp]),
+                                  _vp, _i64, _i32, _i32, _f64, _f64, _f64, _f64, _i32, _vp, _i32, _vp]),
     "cnmf_counter_words": (_i64, []),
-    "cnmf_set_persist_variant": (_i32, [_i32]),
-    "cnmf_get_persist_variant": (_i32, []),
-    "cnmf_set_persist_dyn_frac": (_i32, [ctypes.c_double]),
     "cnmf_wmu_pass_blocks": (_i64, [_i64, _i32, _i32]),
     "cnmf_wmu_sample_pass": (_i32, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_wmu_basis_update": (_i32, [_vp, _vp, _i32, _i32, _vp]),
@@ -82,11 +78,13 @@ _SIGS = {
                                          _i64, _i32, _i32, _f64, _f64, _vp, _vp, _i32, _vp]),
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
-                                  _i32, _f64, _f64, _f64, _f64, _i32, _vp]),
+                                  _i32, _f64, _f64, _f64, _f64, _i32, _i32, _vp]),
     "cnmf_xbuf_bytes": (_i64, [_i32]),
     "cnmf_xbuf_handle_bytes": (_i32, []),
     "cnmf_device_pci_bus_id": (_i32, [_i32, ctypes.c_char_p, _i32]),
     "cnmf_device_can_access_peer": (_i32, [_i32, _i32]),
+    "cnmf_enable_peer_access": (_i32, [_i32, _i32]),
+    "cnmf_persist_workgroups": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32]),
     "cnmf_xbuf_alloc": (_i32, [_i32, ctypes.POINTER(_vp), _vp]),
     "cnmf_xbuf_open": (_i32, [_vp, ctypes.POINTER(_vp)]),
     "cnmf_xbuf_close": (_i32, [_vp]),
@@ -99,12 +97,12 @@ _SIGS = {
     "cnmf_init_stats_rows": (_i64, [_i64]),
     "cnmf_init_stats": (_i32, [_vp, _i64, _i32, _vp, _i64, _vp]),
     "cnmf_init_fill": (_i32, [_vp, _i64, _i32, _vp, _vp, _vp, _f64, _f64, _vp, _i32, _vp]),
-    "cnmf_persist_describe": (_i32, [_i64, _i32, _i32, _i32, ctypes.c_char_p, _i32]),
+    "cnmf_persist_describe": (_i32, [_i64, _i32, _i32, _i32, _i32, ctypes.c_char_p, _i32]),
     "cnmf_host_register": (_i32, [_vp, _i64]),
     "cnmf_host_unregister": (_i32, [_vp]),
     "cnmf_copy_h2d_async": (_i32, [_vp, _vp, _i64, _vp]),
     "cnmf_mu_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
-                                        _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _vp, _i32,
+                                        _i64, _i32, _i32, _f64, _f64, _f64, _f64, _vp, _i32, _vp, _i32,
                                         _vp]),
 }
 

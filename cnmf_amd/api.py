@@ -60,7 +60,7 @@ def _check_X(X):
             X = X.to(torch.float64)
         if not bool(torch.isfinite(X).all()):
             raise ValueError("Input X contains NaN or infinity.")
-        return X
+        return X if X.device.type != "cpu" else X.contiguous()  # host rows are streamed / copied row-major
     X = np.asarray(X)
     if X.ndim != 2:
         raise ValueError(f"Expected 2D array, got {X.ndim}D array instead")
@@ -209,10 +209,27 @@ def _streamed(X, as_torch, memory_budget, solver, Mw):
     return True  # below this the host init costs less than a device round trip
 
 
-def _initial_factors(X, k, init, random_state, device, as_torch, group, host_only=False):
-    """_initialize_nmf (SK:221-373).  The NNDSVD family on a tall X of one process runs its
-    passes over X on the GPU (cnmf_amd.gpu_init, §8 f4); small X, 'random', k > 16 or F > 96, and
-    sharded fits (whose X is one shard of the global matrix) take the host restatement."""
+def _validate_init_device(init_device):
+    if init_device not in ("auto", "host", "gpu"):
+        raise ValueError(f"The 'init_device' parameter must be a str among {{'auto', 'host', 'gpu'}}. "
+                         f"Got {init_device!r} instead.")
+
+
+def _initial_factors(X, k, init, random_state, device, as_torch, group, host_only=False,
+                     init_device="auto"):
+    """_initialize_nmf (SK:221-373).
+
+    init_device='host': the host restatement (cnmf_amd.init), bit-identical to sklearn's
+    _initialize_nmf on the same BLAS (pinned by tests/golden/init_*.npz).
+    init_device='gpu': the NNDSVD family's passes over X on the GPU (cnmf_amd.gpu_init, §8 f4) for a
+    tall X of one process (>= GPU_INIT_MIN_ROWS rows, F <= 96, k <= 16); its range finder works in
+    fp64 on the Gram matrix, so for float32 X it does NOT reproduce sklearn's float32 randomized SVD:
+    on ill-conditioned trailing directions the starts differ at the 1e-3 level (measured: 1.4e-3
+    relative on W at 1e6 synthetic rows, tests/test_gpu_init.py), and so do the fitted factors.
+    init_device='auto' (default): the GPU init for float64 X (where it agrees with sklearn's fp64
+    answer to ~1e-8), the host restatement for float32 / bfloat16 X, so that the default fit
+    reproduces the reference's factors.  'random', small X, sharded fits (X is one shard of the
+    global matrix) and out-of-core fits always take the host restatement."""
     torch = _torch()
     from . import gpu_init as _gpu_init
     if not _TORCH_DT:
@@ -221,9 +238,10 @@ def _initial_factors(X, k, init, random_state, device, as_torch, group, host_onl
     resolved = init
     if init is None:
         resolved = "nndsvda" if k <= min(n_samples, n_features) else "random"
-    if (group is None and not host_only and n_samples >= GPU_INIT_MIN_ROWS and X.min() >= 0
-            and _gpu_init.gpu_init_eligible(n_samples, n_features, k, resolved,
-                                            X.dtype if as_torch else _TORCH_DT.get(X.dtype.type))):
+    xdt = X.dtype if as_torch else _TORCH_DT.get(X.dtype.type)
+    want_gpu = init_device == "gpu" or (init_device == "auto" and xdt == torch.float64)
+    if (want_gpu and group is None and not host_only and n_samples >= GPU_INIT_MIN_ROWS
+            and X.min() >= 0 and _gpu_init.gpu_init_eligible(n_samples, n_features, k, resolved, xdt)):
         dev = torch.device(device) if device is not None else (
             X.device if as_torch and X.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device()))
         Xd = (X if as_torch else torch.from_numpy(X)).to(dev).contiguous()
@@ -232,14 +250,13 @@ def _initial_factors(X, k, init, random_state, device, as_torch, group, host_onl
     return _init.initialize_nmf(Xh, k, init=init, random_state=random_state)
 
 
-def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
-                   l1_ratio, random_state, verbose, device, group=None, return_plan=False,
-                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None,
-                   memory_budget=None):
-    """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
+def _resolve(X, W, H, n_components, init, update_H, alpha_W, alpha_H, l1_ratio, random_state, device,
+             group=None, solver="mu", normalise=None, weights=None, memory_budget=None,
+             init_device="auto"):
+    """Validation, k, the starting factors and the regularisation of `_BaseNMF._fit_transform`
+    (SK:1638-1712, _check_w_h SK:1194-1252, _compute_regularization SK:1254-1265).  Returns
+    (X, Mw, as_torch, streamed, k, W, H, regs); W is None for the update_H=False start."""
     torch = _torch()
-    from .solver import ALSPlan, MUPlan, WeightedMUPlan, run_mu
-
     X = _check_X(X)
     Mw = _validate_weights(weights, X, solver, alpha_W, alpha_H, normalise)
     as_torch = _is_torch(X)
@@ -279,51 +296,97 @@ def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W
                           "use them as initialization.", RuntimeWarning)
         if k == "auto":
             k = n_features
-        W, H = _initial_factors(X, int(k), init, random_state, device, as_torch, group, host_only=streamed)
+        W, H = _initial_factors(X, int(k), init, random_state, device, as_torch, group, host_only=streamed,
+                                init_device=init_device)
     k = int(k)
     if k > 16:
         raise ValueError(f"n_components={k} is not supported: the MI355X kernels handle 1..16.")
     if solver == "als" and k > 4:
         raise ValueError(f"n_components={k} is not supported by solver='als' (1..4).")
-
+    if Mw is not None and k > 8:
+        raise ValueError(f"n_components={k} is not supported by the weighted MU (1..8).")
     regs = _compute_regularization(n_samples, n_features, alpha_W, alpha_H, l1_ratio)
-    dev = torch.device(device) if device is not None else (
-        X.device if as_torch and X.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device()))
+    return X, Mw, as_torch, streamed, k, W, H, regs
+
+
+def _make_plan(X, Mw, k, regs, dev, *, solver="mu", sum_to_one=None, smoothness=0.0, group=None,
+               streamed=False, memory_budget=None):
+    """The plan (device state + launches) that runs the fit of X (all of it, or one shard)."""
+    torch = _torch()
+    from .solver import ALSPlan, MUPlan, WeightedMUPlan
     if streamed:  # §8 f3: X stays in host memory and streams through a memory_budget of HBM
         from .outofcore import StreamedMUPlan
-        plan = StreamedMUPlan(X, k, regs[0], regs[2], regs[1], regs[3], group=group, device=dev,
+        return StreamedMUPlan(X, k, regs[0], regs[2], regs[1], regs[3], group=group, device=dev,
                               memory_budget=memory_budget)
-    else:
-        Xd = X if as_torch else torch.from_numpy(X)
-        Xd = Xd.to(dev, non_blocking=False).contiguous()
-        if Mw is not None:
-            if k > 8:
-                raise ValueError(f"n_components={k} is not supported by the weighted MU (1..8).")
-            Md = (Mw if _is_torch(Mw) else torch.from_numpy(Mw)).to(dev, torch.float32).contiguous()
-            plan = WeightedMUPlan(Xd, Md, k, group=group)
-        elif solver == "als":
-            plan = ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
-        else:
-            plan = MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
-    if W is None:  # update_H=False start: sqrt(X.mean()/k) in X's dtype (SK:1228-1232)
-        if as_torch:
-            avg = float(torch.sqrt(X.double().mean() / k))
-        else:
-            avg = float(np.sqrt(X.mean() / k))
+    Xd = X if _is_torch(X) else torch.from_numpy(np.ascontiguousarray(X))
+    Xd = Xd.to(dev, non_blocking=False).contiguous()
+    if Mw is not None:
+        Md = (Mw if _is_torch(Mw) else torch.from_numpy(np.ascontiguousarray(Mw))).to(dev, torch.float32).contiguous()
+        return WeightedMUPlan(Xd, Md, k, group=group)
+    if solver == "als":
+        return ALSPlan(Xd, k, sum_to_one=sum_to_one, smoothness=smoothness, group=group)
+    return MUPlan(Xd, k, regs[0], regs[2], regs[1], regs[3], group=group)
+
+
+def _start(plan, W, H, avg):
+    """Load the starting factors; W None: the update_H=False start sqrt(X.mean()/k) (SK:1228-1232)."""
+    torch = _torch()
+    if W is None:
         plan.W.fill_(avg)
     else:
         plan.set_W(W if _is_torch(W) else torch.from_numpy(np.ascontiguousarray(W)))
     plan.set_H(H if _is_torch(H) else torch.from_numpy(np.ascontiguousarray(H)))
-    n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H, verbose=verbose)
-    if n_iter == max_iter and tol > 0:
-        warnings.warn("Maximum number of iterations %d reached. Increase it to improve "
-                      "convergence." % max_iter, ConvergenceWarning)
-    if normalise is not None and update_H:
-        plan.normalise(normalise)  # §8 a6: unit-norm basis rows, scales folded into W
-    Wd, Hd = plan.W, plan.H()
-    if return_plan:
-        return Wd, Hd, n_iter, plan, as_torch, X
-    return _out(Wd, as_torch, X), _out(Hd, as_torch, X), n_iter
+
+
+def _transform_start(X, as_torch, k):
+    """sqrt(X.mean() / k) in X's dtype (SK:1228-1232)."""
+    if as_torch:
+        return float(_torch().sqrt(X.double().mean() / k))
+    return float(np.sqrt(X.mean() / k))
+
+
+def _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
+                   l1_ratio, random_state, verbose, device, group=None, return_plan=False,
+                   normalise=None, solver="mu", sum_to_one=None, smoothness=0.0, weights=None,
+                   memory_budget=None, init_device="auto"):
+    """`_BaseNMF._fit_transform` for solver='mu' (SK:1638-1734) on the MI355X path."""
+    torch = _torch()
+    from .solver import run_mu
+
+    X, Mw, as_torch, streamed, k, W, H, regs = _resolve(
+        X, W, H, n_components, init, update_H, alpha_W, alpha_H, l1_ratio, random_state, device,
+        group=group, solver=solver, normalise=normalise, weights=weights, memory_budget=memory_budget,
+        init_device=init_device)
+    dev = torch.device(device) if device is not None else (
+        X.device if as_torch and X.device.type == "cuda" else torch.device("cuda", torch.cuda.current_device()))
+    plan = _make_plan(X, Mw, k, regs, dev, solver=solver, sum_to_one=sum_to_one, smoothness=smoothness,
+                      group=group, streamed=streamed, memory_budget=memory_budget)
+    _start(plan, W, H, _transform_start(X, as_torch, k) if W is None else None)
+    try:
+        n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H, verbose=verbose)
+        if n_iter == max_iter and tol > 0:
+            warnings.warn("Maximum number of iterations %d reached. Increase it to improve "
+                          "convergence." % max_iter, ConvergenceWarning)
+        if normalise is not None and update_H:
+            plan.normalise(normalise)  # §8 a6: unit-norm basis rows, scales folded into W
+        Wd, Hd = plan.W, plan.H()
+        if return_plan:  # the caller releases the plan (NMF: after reconstruction_err_)
+            return Wd, Hd, n_iter, plan, as_torch, X
+        return _out(Wd, as_torch, X), _out(Hd, as_torch, X), n_iter
+    except BaseException:
+        _release(plan)
+        raise
+    finally:
+        if not return_plan:
+            _release(plan)
+
+
+def _release(plan):
+    """Unpin a streamed plan's host X and unmap exchange buffers now, not at garbage collection
+    (a plan kept alive by a traceback would keep the caller's memory page-locked)."""
+    rel = getattr(plan, "release", None)
+    if rel is not None:
+        rel()
 
 
 def _out(t, as_torch, X):
@@ -335,7 +398,8 @@ def _out(t, as_torch, X):
 def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=True, solver="mu",
               beta_loss="frobenius", tol=1e-4, max_iter=200, alpha_W=0.0, alpha_H="same",
               l1_ratio=0.0, random_state=None, verbose=0, shuffle=False, device=None,
-              normalise=None, sum_to_one=None, smoothness=0.0, weights=None, memory_budget=None):
+              normalise=None, sum_to_one=None, smoothness=0.0, weights=None, memory_budget=None,
+              init_device="auto", devices=None):
     """Compute NMF X ≈ W·H with the multiplicative-update solver on an MI355X.
 
     Same signature, argument meaning, return value (W, H, n_iter) and errors as
@@ -355,14 +419,29 @@ def factorise(X, W=None, H=None, n_components="auto", *, init=None, update_H=Tru
     `memory_budget` (bytes; None = off): a host X (NumPy array, memory map or CPU tensor) larger
     than this is not copied to the GPU whole but streamed through HBM in row chunks every iteration
     (cnmf_amd.outofcore); same factors as the in-HBM fit up to fp summation order.
+    `init_device` ('auto' | 'host' | 'gpu'): where init=None / 'nndsvd*' computes its SVD start —
+    see `_initial_factors`; 'auto' reproduces sklearn's start for float32 X (host restatement) and
+    runs the passes over X on the GPU for float64 X.
+    `devices` (list of HIP device indices or torch devices; None = one device): split the rows
+    over several GPUs driven from THIS process (cnmf_amd.multidevice): one stream and
+    one persistent launch per device per stretch, the per-device [WᵀX | WᵀW] summed inside the
+    launches over peer-mapped buffers.  Same factors as the one-device fit to fp64 summation order.
     """
     _validate_params(n_components, init, solver, beta_loss, tol, max_iter, alpha_W, alpha_H, l1_ratio)
     _validate_normalise(normalise)
     _validate_als(solver, alpha_W, alpha_H, sum_to_one, smoothness)
+    _validate_init_device(init_device)
+    if devices is not None:
+        from .multidevice import factorise_devices
+        return factorise_devices(X, W, H, n_components, devices=devices, init=init, update_H=update_H,
+                                 solver=solver, tol=tol, max_iter=max_iter, alpha_W=alpha_W,
+                                 alpha_H=alpha_H, l1_ratio=l1_ratio, random_state=random_state,
+                                 verbose=verbose, normalise=normalise, sum_to_one=sum_to_one,
+                                 smoothness=smoothness, weights=weights, init_device=init_device)
     return _fit_transform(X, W, H, n_components, init, update_H, tol, max_iter, alpha_W, alpha_H,
                           l1_ratio, random_state, verbose, device, normalise=normalise,
                           solver=solver, sum_to_one=sum_to_one, smoothness=smoothness,
-                          weights=weights, memory_budget=memory_budget)
+                          weights=weights, memory_budget=memory_budget, init_device=init_device)
 
 
 def _validate_normalise(normalise):
@@ -385,8 +464,9 @@ class NMF:
     def __init__(self, n_components="auto", *, init=None, solver="mu", beta_loss="frobenius",
                  tol=1e-4, max_iter=200, random_state=None, alpha_W=0.0, alpha_H="same",
                  l1_ratio=0.0, verbose=0, shuffle=False, device=None, normalise=None,
-                 sum_to_one=None, smoothness=0.0, memory_budget=None):
+                 sum_to_one=None, smoothness=0.0, memory_budget=None, init_device="auto"):
         self.n_components = n_components
+        self.init_device = init_device
         self.memory_budget = memory_budget
         self.normalise = normalise
         self.sum_to_one = sum_to_one
@@ -408,7 +488,8 @@ class NMF:
         return {k: getattr(self, k) for k in ("n_components", "init", "solver", "beta_loss", "tol",
                                               "max_iter", "random_state", "alpha_W", "alpha_H",
                                               "l1_ratio", "verbose", "shuffle", "device",
-                                              "normalise", "sum_to_one", "smoothness", "memory_budget")}
+                                              "normalise", "sum_to_one", "smoothness", "memory_budget",
+                                              "init_device")}
 
     def set_params(self, **params):
         for k, v in params.items():
@@ -420,6 +501,7 @@ class NMF:
                          self.max_iter, self.alpha_W, self.alpha_H, self.l1_ratio)
         _validate_normalise(self.normalise)
         _validate_als(self.solver, self.alpha_W, self.alpha_H, self.sum_to_one, self.smoothness)
+        _validate_init_device(self.init_device)
 
     def fit_transform(self, X, y=None, W=None, H=None, weights=None):
         """SK:1600-1636: learn the model, return W; sets reconstruction_err_ from the final W, H
@@ -430,13 +512,18 @@ class NMF:
             self.alpha_H, self.l1_ratio, self.random_state, self.verbose, self.device,
             return_plan=True, normalise=self.normalise, solver=self.solver,
             sum_to_one=self.sum_to_one, smoothness=self.smoothness, weights=weights,
-            memory_budget=self.memory_budget)
-        self.reconstruction_err_ = plan.frobenius_error()
+            memory_budget=self.memory_budget, init_device=self.init_device)
+        try:
+            self.reconstruction_err_ = plan.frobenius_error()
+            Wout = _out(Wd, as_torch, Xc)
+            Hout = _out(Hd, as_torch, Xc)
+        finally:
+            _release(plan)
         self.n_components_ = int(Hd.shape[0])
-        self.components_ = _out(Hd, as_torch, Xc)
+        self.components_ = Hout
         self.n_iter_ = n_iter
         self.n_features_in_ = int(Xc.shape[1])
-        return _out(Wd, as_torch, Xc)
+        return Wout
 
     def fit(self, X, y=None, **params):
         self.fit_transform(X, **params)

@@ -65,6 +65,18 @@ static int set_err(int code, const char* fmt, ...) {
   return code;
 }
 
+// Diagnostic switches (A/B timing and tools/ probes) are read from the environment only in the
+// diagnostic build (-DCNMF_DIAG: python -m cnmf_amd.build --diag); the product library ignores the
+// environment, so every plan's behaviour follows from its arguments alone.
+static const char* diag_env(const char* name) {
+#ifdef CNMF_DIAG
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+
 #define HIP_CHECK(expr)                                                                   \
   do {                                                                                    \
     hipError_t e_ = (expr);                                                               \
@@ -3977,6 +3989,7 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
 // HBM read probe: the achievable streaming-read ceiling on this device (16-byte loads, 8 in flight
 // per lane, grid-stride; one fp64 checksum per workgroup so nothing is dead code).
 // ------------------------------------------------------------------------------------------------
+#ifdef CNMF_DIAG
 __global__ __launch_bounds__(256) void hbm_probe_kernel(const u32x4* __restrict__ buf, int64_t n16,
                                                         double* __restrict__ out) {
   const int64_t stride = (int64_t)gridDim.x * 256;
@@ -4002,6 +4015,7 @@ __global__ __launch_bounds__(256) void hbm_probe_kernel(const u32x4* __restrict_
     out[blockIdx.x] = (double)a;
   }
 }
+#endif
 
 // ------------------------------------------------------------------------------------------------
 // host side: kernel selection, occupancy-derived grid, launches
@@ -4086,9 +4100,9 @@ static constexpr size_t kMaxLds = 160 * 1024;
 // A/B switches for benchmarking: CNMF_PASS_KERNEL=valu|mfma|sl restricts the accumulating pass to
 // one kernel family (CNMF_FORCE_VALU=1 is the older spelling of "valu")
 static const char* pass_choice() {
-  const char* e = getenv("CNMF_PASS_KERNEL");
+  const char* e = diag_env("CNMF_PASS_KERNEL");
   if (e && *e) return e;
-  return getenv("CNMF_FORCE_VALU") ? "valu" : "";
+  return diag_env("CNMF_FORCE_VALU") ? "valu" : "";
 }
 static bool g_force_valu = strcmp(pass_choice(), "valu") == 0;
 static bool g_no_sl = strcmp(pass_choice(), "valu") == 0 || strcmp(pass_choice(), "mfma") == 0;
@@ -5487,7 +5501,7 @@ static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy
 
 extern "C" {
 
-int cnmf_abi_version(void) { return 201; }
+int cnmf_abi_version(void) { return 300; }
 
 const char* cnmf_last_error(void) { return g_err; }
 
@@ -5823,6 +5837,7 @@ int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
 }
 #endif
 
+#ifdef CNMF_DIAG
 int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream) {
   if (!buf || !out || bytes < 16 || n_blocks < 1)
     return set_err(CNMF_ERR_ARG, "invalid hbm probe arguments");
@@ -5833,13 +5848,14 @@ int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, vo
   HIP_CHECK(hipGetLastError());
   return CNMF_OK;
 }
+#endif
 
 // The persistent path serves fp32 X at F = 81, k = 4 with whole tiles and >= 3 tiles per workgroup
 // (CNMF_PERSIST=0 disables it for A/B timing).  Returns its grid, 0 when not eligible, < 0 on error.
-static bool g_no_persist = getenv("CNMF_PERSIST") && strcmp(getenv("CNMF_PERSIST"), "0") == 0;
+static bool g_no_persist = diag_env("CNMF_PERSIST") && strcmp(diag_env("CNMF_PERSIST"), "0") == 0;
 // prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2); CNMF_WRES=0 keeps W streaming
-static int g_persist_pd = (getenv("CNMF_PERSIST_PD") && atoi(getenv("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
-static bool g_no_wres = getenv("CNMF_WRES") && strcmp(getenv("CNMF_WRES"), "0") == 0;
+static int g_persist_pd = (diag_env("CNMF_PERSIST_PD") && atoi(diag_env("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
+static bool g_no_wres = diag_env("CNMF_WRES") && strcmp(diag_env("CNMF_WRES"), "0") == 0;
 static PassFn persist_fn(bool wres = false, bool multi = false) {
   if (multi)  // the multi-GPU launch: PD = 2 only
     return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true>)
@@ -5876,26 +5892,28 @@ static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
   return (with > 0 && with >= base) ? lds : 0;
 }
 
-// ---- the two-team variant (mu_iter_sl_kernel<2, true, MULTI, 2>: one 8-wave workgroup per CU, W
-// resident): multi-iteration launches of a shape whose W tiles fit in LDS twice over.  Which of the
-// two layouts is faster differs between boxes (same-box A/B, 500-iteration launches: 64.4 vs
-// 66.5 µs on one, 70.2 vs 67.3 µs on another), so it is a process-wide switch the host can set
-// after timing both (MUPlan.tune): 1 = pairs of 4-wave workgroups (the default), 2 = two teams.
-// CNMF_TEAMS=1|2 sets the initial value.
-static int initial_variant() {
-  const char* v = getenv("CNMF_PERSIST_VARIANT");
+// ---- layouts of the persistent MU launch (the `layout` argument of cnmf_mu_iterations /
+// cnmf_mu_iterations_multi / cnmf_mu_shard_step / cnmf_persist_describe; chosen per plan, never
+// process-wide): 4 = barrier-free wave tiles (mu_iter_wt_kernel, the default), 1 = pairs of 4-wave
+// workgroups per CU, 2 = one 8-wave two-team workgroup per CU, 3 = pairs with floating tiles.  Which
+// of 4 / 1 / 2 is fastest has differed between boxes, so MUPlan.tune() times them and keeps the
+// fastest for its plan.  0 = the default (4; CNMF_PERSIST_VARIANT / CNMF_TEAMS in the diagnostic build).
+static int default_layout() {
+  const char* v = diag_env("CNMF_PERSIST_VARIANT");
   if (v && atoi(v) >= 1 && atoi(v) <= 4) return atoi(v);
-  return (getenv("CNMF_TEAMS") && strcmp(getenv("CNMF_TEAMS"), "2") == 0) ? 2 : 4;
+  return (diag_env("CNMF_TEAMS") && strcmp(diag_env("CNMF_TEAMS"), "2") == 0) ? 2 : 4;
 }
-static std::atomic<int> g_persist_variant{initial_variant()};
-
-int cnmf_set_persist_variant(int v) {
-  if (v < 1 || v > 4)
-    return set_err(CNMF_ERR_ARG, "variant must be 1 (pairs), 2 (teams), 3 (pairs + floating tiles) or 4 (wave tiles)");
-  g_persist_variant.store(v);
-  return CNMF_OK;
+static int resolve_layout(int layout) {
+  if (layout == 0) return default_layout();
+  return (layout >= 1 && layout <= 4) ? layout : -1;
 }
-int cnmf_get_persist_variant(void) { return g_persist_variant.load(); }
+#define RESOLVE_LAYOUT(var)                                                                                  \
+  do {                                                                                                      \
+    var = resolve_layout(var);                                                                              \
+    if (var < 0)                                                                                            \
+      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles) " \
+                     "or 4 (wave tiles)");                                                                  \
+  } while (0)
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 2>);
@@ -5905,22 +5923,21 @@ static PassFn persist_teams_fn(bool multi) {
 // workgroup keeps floor(frac · n_tiles / G) tiles resident (frac = CNMF_DYN_FRAC, default 0.8), the
 // rest are drawn from a pool every iteration.  Returns the static tiles per workgroup (0: not
 // eligible) and the LDS bytes.
-static std::atomic<double> g_dyn_frac{getenv("CNMF_DYN_FRAC") ? atof(getenv("CNMF_DYN_FRAC")) : 0.8};
-int cnmf_set_persist_dyn_frac(double frac) {
-  if (!(frac > 0.0 && frac <= 1.0)) return set_err(CNMF_ERR_ARG, "frac must lie in (0, 1]");
-  g_dyn_frac = frac;
-  return CNMF_OK;
+// the resident fraction of layout 3 (CNMF_DYN_FRAC in the diagnostic build)
+static double dyn_frac() {
+  const char* v = diag_env("CNMF_DYN_FRAC");
+  const double fr = v ? atof(v) : 0.8;
+  return fr > 0.0 && fr <= 1.0 ? fr : 0.8;
 }
-static bool g_dyn_multi = getenv("CNMF_DYN_MULTI") && strcmp(getenv("CNMF_DYN_MULTI"), "1") == 0;
+static bool g_dyn_multi = diag_env("CNMF_DYN_MULTI") && strcmp(diag_env("CNMF_DYN_MULTI"), "1") == 0;
 static PassFn persist_dyn_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 1, true>)
                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 1, true>);
 }
-static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, size_t* lds_out) {
-  if (g_persist_variant.load() != 3 || g_no_wres || g_persist_pd != 2 || G <= 0) return 0;
+static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, int layout, size_t* lds_out) {
+  if (layout != 3 || g_no_wres || g_persist_pd != 2 || G <= 0) return 0;
   if (multi && !g_dyn_multi) return 0;  // the multi-GPU launch keeps layout 1 unless CNMF_DYN_MULTI=1
-  const double fr = g_dyn_frac.load();
-  const double frac = fr > 0.0 && fr <= 1.0 ? fr : 0.8;
+  const double frac = dyn_frac();
   const int64_t S = (int64_t)(frac * (double)n_tiles / (double)G);
   if (S < 4 || S * G > n_tiles) return 0;  // >= PD + 2 static tiles (no draw crosses an iteration)
   const size_t lds = (size_t)sl::L_PTOTAL + (size_t)S * sl::WB;
@@ -5931,8 +5948,8 @@ static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, size_t* ld
 }
 
 // workgroups (0: not eligible) and LDS bytes of a two-team launch over n_tiles (persist_grid > 0)
-static int64_t persist_teams_grid(int64_t n_tiles, bool multi, size_t* lds_out) {
-  if (g_persist_variant.load() != 2 || g_no_wres || g_persist_pd != 2) return 0;
+static int64_t persist_teams_grid(int64_t n_tiles, bool multi, int layout, size_t* lds_out) {
+  if (layout != 2 || g_no_wres || g_persist_pd != 2) return 0;
   int dev = 0, ncu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -5955,7 +5972,7 @@ static int64_t persist_teams_grid(int64_t n_tiles, bool multi, size_t* lds_out) 
 // (8-sample tiles); W resident in LDS when the grid's share fits, else streamed with X).
 // CNMF_WT_PD = prefetch depth 2..4 of the k = 4 W-resident single-GPU kernel (default 3).
 static int wt_pd(int k, bool wres, bool multi) {
-  const char* v = getenv("CNMF_WT_PD");
+  const char* v = diag_env("CNMF_WT_PD");
   const int pd = v ? atoi(v) : 3;
   return (k == 4 && wres && !multi && pd >= 2 && pd <= 4) ? pd : 3;
 }
@@ -5987,9 +6004,9 @@ struct WtLaunch {
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
-static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, WtLaunch* out) {
+static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, WtLaunch* out) {
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
-  if (k == 4 && g_persist_variant.load() != 4) return false;
+  if (k == 4 && layout != 4) return false;
   const int tsw = 64 / k, wbw = tsw * k * 4;
   if (n_rows % tsw != 0) return false;
   const size_t l_wres = k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES;
@@ -6019,7 +6036,7 @@ struct WwLaunch {
 static bool ww_plan(int64_t n_rows, int F, int k, WwLaunch* out, bool multi = false) {
   constexpr int PD = 2;
   if (F != wt::F || k != ww::K || n_rows <= 0 || n_rows % ww::TSW != 0) return false;
-  if (getenv("CNMF_WMU_PERSIST") && atoi(getenv("CNMF_WMU_PERSIST")) == 0) return false;
+  if (diag_env("CNMF_WMU_PERSIST") && atoi(diag_env("CNMF_WMU_PERSIST")) == 0) return false;
   const int64_t n_tiles = n_rows / ww::TSW;
   const int64_t G = std::min<int64_t>({(int64_t)device_cus(), n_tiles / (wt::NWV * (PD + 1)),
                                        (int64_t)sl::GROUP * sl::MAX_GROUPS});
@@ -6043,7 +6060,7 @@ struct WaLaunch {
 // fp64 and LDS latencies of the W-step, at 256 registers per lane and PD = 2; measured on one box,
 // cfg5: 146.6 us per iteration at 1, 123.1 us at 2, profiles/r02/session5/als_iter)
 static int wa_occ() {
-  static const int v = getenv("CNMF_ALS_OCC") && atoi(getenv("CNMF_ALS_OCC")) == 1 ? 1 : 2;
+  static const int v = diag_env("CNMF_ALS_OCC") && atoi(diag_env("CNMF_ALS_OCC")) == 1 ? 1 : 2;
   return v;
 }
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
@@ -6057,7 +6074,7 @@ static PassFn wa_fn(bool multi = false) {
 static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false) {
   const int PD = wa_pd();
   if (x_dtype != CNMF_F32 || F != wt::F || k != wa::K || n_rows <= 0 || n_rows % wa::TSW != 0) return false;
-  if (getenv("CNMF_ALS_PERSIST") && atoi(getenv("CNMF_ALS_PERSIST")) == 0) return false;
+  if (diag_env("CNMF_ALS_PERSIST") && atoi(diag_env("CNMF_ALS_PERSIST")) == 0) return false;
   const int64_t n_tiles = n_rows / wa::TSW;
   const int64_t G = std::min<int64_t>({(int64_t)device_cus() * wa_occ(), n_tiles / (wt::NWV * (PD + 1)),
                                        (int64_t)sl::GROUP * sl::MAX_GROUPS});
@@ -6165,17 +6182,26 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   return CNMF_OK;
 }
 
+int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int layout, int multi) {
+  RESOLVE_LAYOUT(layout);
+  WtLaunch L;
+  if (wt_plan(n_rows, x_dtype, n_features, k, multi != 0, layout, &L)) return L.G;
+  const int64_t g = persist_grid(n_rows, x_dtype, n_features, k, multi != 0);
+  return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : g;
+}
+
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   WtLaunch L;
-  if (wt_plan(n_rows, x_dtype, n_features, k, false, &L)) return 1;
+  if (wt_plan(n_rows, x_dtype, n_features, k, false, 4, &L)) return 1;
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
 }
 
-int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, char* out, int len) {
+int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, int layout, char* out, int len) {
   if (!out || len < 1) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  RESOLVE_LAYOUT(layout);
   WtLaunch L;
-  if (wt_plan(n_rows, x_dtype, n_features, k, false, &L)) {
+  if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L)) {
     const bool wres = L.lds > (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES);
     snprintf(out, (size_t)len,
              "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
@@ -6191,7 +6217,7 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, ch
   }
   static const char* names[] = {"", "pairs of 4-wave workgroups per CU", "one 8-wave two-team workgroup per CU",
                                 "pairs of 4-wave workgroups per CU with floating tiles"};
-  const int v = g_persist_variant.load();
+  const int v = layout;
   snprintf(out, (size_t)len, "mu_iter_sl_kernel: %s (%lld workgroups)", (v >= 1 && v <= 3) ? names[v] : "?",
            (long long)g);
   return 1;
@@ -6244,6 +6270,22 @@ int cnmf_device_can_access_peer(int device, int peer) {
   return ok ? 1 : 0;
 }
 
+int cnmf_enable_peer_access(int device, int peer) {
+  if (device == peer) return CNMF_OK;
+  int cur = 0;
+  HIP_CHECK(hipGetDevice(&cur));
+  HIP_CHECK(hipSetDevice(device));
+  hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // already mapped: not an error, and not left sticky
+    e = hipSuccess;
+  }
+  const hipError_t e2 = hipSetDevice(cur);
+  if (e != hipSuccess) return set_err(CNMF_ERR_HIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", device, peer, hipGetErrorString(e));
+  if (e2 != hipSuccess) return set_err(CNMF_ERR_HIP, "hipSetDevice: %s", hipGetErrorString(e2));
+  return CNMF_OK;
+}
+
 // ---- host-resident X (out-of-core fits: cnmf_amd/outofcore.py)
 int cnmf_host_register(void* ptr, int64_t bytes) {
   if (!ptr || bytes <= 0) return set_err(CNMF_ERR_ARG, "null pointer or empty range");
@@ -6291,7 +6333,7 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
                              double* HHt, double* partials, int64_t n_parts, double* stage,
                              uint32_t* counter, double* AB, int64_t n_rows, double l1_W, double l2_W,
                              double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s,
-                             uint64_t* xctl = nullptr) {
+                             int layout, uint64_t* xctl = nullptr) {
   if (G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
                                   (long long)n_parts, (long long)G);
   PersistArgs pa;
@@ -6319,14 +6361,14 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   void* args[] = {&pa};
   if (n_iter > 1) {
     size_t tlds = 0;
-    const int64_t GT = persist_teams_grid(n_rows / TS, multi, &tlds);
+    const int64_t GT = persist_teams_grid(n_rows / TS, multi, layout, &tlds);
     if (GT > 0 && GT <= n_parts) {
       pa.n_groups = (int)((GT + sl::GROUP - 1) / sl::GROUP);
       HIP_CHECK(hipLaunchKernel(persist_teams_fn(multi), dim3((unsigned)GT), dim3(2 * NT), args, tlds, s));
       return CNMF_OK;
     }
     size_t dlds = 0;
-    const int S = persist_dyn_static(n_rows / TS, G, multi, &dlds);
+    const int S = persist_dyn_static(n_rows / TS, G, multi, layout, &dlds);
     if (S > 0) {
       pa.n_static = S;
       HIP_CHECK(hipLaunchKernel(persist_dyn_fn(multi), dim3((unsigned)G), dim3(NT), args, dlds, s));
@@ -6348,8 +6390,9 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
 int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
                        double* partials, int64_t n_parts, double* stage, uint32_t* counter, double* AB,
                        int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
-                       double l2_H, int apply_first, void* stream) {
+                       double l2_H, int apply_first, int layout, void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  RESOLVE_LAYOUT(layout);
   if ((n_rows > 0 && (!X || !W)) || !H64 || !Ht || !HHt || !stage || !counter || !AB)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
   if (n_rows == 0) {  // an empty shard (world > rows): the pending update, then zeros for the all-reduce
@@ -6363,7 +6406,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
   {  // one wave-tile launch with n_iter = 1: the multi-iteration launch's layout, so the RCCL path
      // and the in-launch exchange sum the same partials; only tickets, no waits
     WtLaunch L;
-    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, &L) && L.G <= n_parts)
+    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts)
       return launch_wt(L, 1, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
                        apply_first, 0, hs, nullptr);
   }
@@ -6424,12 +6467,13 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
-                       void* const* events, int n_events, void* stream) {
+                       int layout, void* const* events, int n_events, void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   if (n_iter <= 0) return CNMF_OK;
+  RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan(n_rows, x_dtype, n_features, k, false, &L) && L.G <= n_parts) {
+    if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
       if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
@@ -6449,7 +6493,7 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
       return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
     if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
     int st = launch_persistent(G, n_iter, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB,
-                               n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs);
+                               n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs, layout);
     if (st) return st;
     if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
     return CNMF_OK;
@@ -6494,13 +6538,14 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
                              double* Ht, double* HHt, double* partials, int64_t n_parts,
                              double* stage, uint32_t* counter, double* AB, int64_t n_rows,
                              int n_features, int k, double l1_W, double l2_W, double l1_H,
-                             double l2_H, uint64_t* xctl, void* const* events, int n_events,
+                             double l2_H, uint64_t* xctl, int layout, void* const* events, int n_events,
                              void* stream) {
   hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
   if (n_iter <= 0) return CNMF_OK;
+  RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan(n_rows, x_dtype, n_features, k, true, &L) && L.G <= n_parts) {
+    if (wt_plan(n_rows, x_dtype, n_features, k, true, layout, &L) && L.G <= n_parts) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
       if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
@@ -6520,7 +6565,7 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   int st = launch_persistent(G, n_iter, X, W, H64, Ht, HHt, partials, n_parts, stage, counter, AB,
-                             n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs, xctl);
+                             n_rows, l1_W, l2_W, l1_H, l2_H, 0, 1, hs, layout, xctl);
   if (st) return st;
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;

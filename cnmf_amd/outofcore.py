@@ -162,6 +162,8 @@ class StreamedMUPlan:
         lo, hi = self.chunks[seq % self.n_chunks]
         nbytes = (hi - lo) * self.F * self.src.dtype.itemsize
         dst = self.bufs[slot]
+        if self.mode == "staged" and self._staging is None:  # after release(): a pinned ring, lazily
+            self._staging = [torch.empty_like(b, device="cpu", pin_memory=True) for b in self.bufs]
         with torch.cuda.stream(self.copy_stream):
             if self._consumed[slot] is not None:
                 self.copy_stream.wait_event(self._consumed[slot])
@@ -243,7 +245,7 @@ class StreamedMUPlan:
             _ptr(Xc), self.xdt, _ptr(self.W[lo:hi]), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
             _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
             _ptr(self.AB_step), hi - lo, self.F, self.k, self.l1_W, self.l2_W, self.l1_H,
-            self.l2_H, 0, self._stream()), "cnmf_mu_shard_step")
+            self.l2_H, 0, 0, self._stream()), "cnmf_mu_shard_step")
         self.AB_chunks[c].copy_(self.AB_step)  # rows of n_out doubles need not be 16-byte aligned
 
     def _chunk_transform(self, c: int, Xc: torch.Tensor):
@@ -316,12 +318,13 @@ class StreamedMUPlan:
         return self.H64.to(dtype or self.tc)
 
     def release(self):
-        """Drain the copies and unlock X's pages (the plan keeps working in staged mode)."""
+        """Drain the copies and unlock X's pages (the plan keeps working in staged mode; its pinned
+        staging ring is allocated only if it streams again)."""
         torch.cuda.synchronize(self.device)
         if self._registered:
             self.lib.cnmf_host_unregister(self.src.ctypes.data)
             self._registered = False
-            self._staging = [torch.empty_like(b, device="cpu", pin_memory=True) for b in self.bufs]
+            self._staging = None
             self.mode = "staged"
 
     def __del__(self):

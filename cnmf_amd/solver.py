@@ -37,7 +37,27 @@ def plan_world(group) -> int:
     (independent per-rank fits under torchrun, e.g. cNMF replicates, must not all-reduce)."""
     if group is None:
         return 1
+    if getattr(group, "is_local", False):  # shards of one process (cnmf_amd.multidevice)
+        return group.size()
     return torch.distributed.get_world_size(group)
+
+
+def collective_tensor(values, group, device):
+    """A float64 tensor of `values` on the device the group's backend reduces (host memory for
+    gloo, the plan's GPU for RCCL)."""
+    dev = "cpu" if torch.distributed.get_backend(group) == "gloo" else device
+    return torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+
+
+def agree_max(values, group, device):
+    """Element-wise maximum of `values` over the ranks of `group` (identity without a group)."""
+    if group is None or plan_world(group) == 1:
+        return [float(v) for v in values]
+    if getattr(group, "is_local", False):
+        return group.all_reduce_values(values, "max")
+    t = collective_tensor(values, group, device)
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX, group=group)
+    return [float(v) for v in t.tolist()]
 
 
 def _event_array(events):
@@ -110,6 +130,7 @@ class MUPlan:
             p = self.lib.cnmf_mu_persistent(self.n_rows, self.F, self.k, self.xdt)
         self.persistent_shape = bool(check(p, "cnmf_mu_persistent"))  # the persistent kernel serves it
         self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
+        self.layout = 0  # layout of the persistent launch (include/cnmf_hip.h; 0 = default); tune() sets it
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
         self.exchange = False  # True: multi-GPU iterations as one launch per rank (enable_exchange)
         self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
@@ -126,6 +147,8 @@ class MUPlan:
         dist = torch.distributed
         if self.group is None:
             raise RuntimeError("enable_exchange needs the plan's torch.distributed group (MUPlan(..., group=...))")
+        if getattr(self.group, "is_local", False):
+            return self._enable_exchange_local()
         rank = dist.get_rank(self.group)
         ok = torch.tensor([1.0 if self.persistent_shape else 0.0])
         handle, ptr, err = None, ctypes.c_void_p(), ""
@@ -185,6 +208,43 @@ class MUPlan:
         self.persistent = True
         self.shard_steps = False
 
+    def _enable_exchange_local(self):
+        """enable_exchange for shards driven by threads of ONE process (cnmf_amd.multidevice): the
+        exchange buffers are mapped directly (peer access enabled between distinct devices), no IPC.
+        Collective over the local group: raises on every shard when any shard cannot take part."""
+        grp = self.group
+        ptr, err = ctypes.c_void_p(), ""
+        if not self.persistent_shape:
+            err = f"shard {grp.rank()}: not a persistent shape"
+        else:
+            hbuf = ctypes.create_string_buffer(int(self.lib.cnmf_xbuf_handle_bytes()))
+            with torch.cuda.device(self.device):
+                if self.lib.cnmf_xbuf_alloc(self.world, ctypes.byref(ptr), hbuf) < 0:
+                    err = self.lib.cnmf_last_error().decode()
+        infos = grp.all_gather((ptr.value, self.device.index, err))
+        errs = [e for _, _, e in infos if e]
+        if not errs:
+            with torch.cuda.device(self.device):
+                for _, d, _ in infos:
+                    if d != self.device.index and self.lib.cnmf_enable_peer_access(self.device.index, d) < 0:
+                        errs.append(f"device {self.device.index} -> {d}: " + self.lib.cnmf_last_error().decode())
+        errs = [e for e in grp.all_gather("; ".join(errs)) if e]
+        if errs:
+            if ptr.value:
+                self.lib.cnmf_xbuf_free(ptr)
+            raise _lib.HipLibraryError("in-launch exchange unavailable: " + "; ".join(errs))
+        peers = [p for p, _, _ in infos]
+        self._xbuf, self._xopened = ptr.value, []
+        self.xctl = torch.zeros(int(check(self.lib.cnmf_xctl_words(self.world), "cnmf_xctl_words")),
+                                dtype=torch.int64, device=self.device)
+        with torch.cuda.device(self.device):
+            check(self.lib.cnmf_xctl_init(_ptr(self.xctl), (ctypes.c_void_p * self.world)(*peers),
+                                          grp.rank(), self.world), "cnmf_xctl_init")
+        self.xrank = grp.rank()
+        self.exchange = True
+        self.persistent = True
+        self.shard_steps = False
+
     def _pci_bus_id(self, dev: int) -> str:
         buf = ctypes.create_string_buffer(64)
         check(self.lib.cnmf_device_pci_bus_id(dev, buf, 64), "cnmf_device_pci_bus_id")
@@ -238,6 +298,9 @@ class MUPlan:
                 self._stream()), "cnmf_mu_sample_pass")
 
     def reduce(self, n_out: int, out: torch.Tensor):
+        if self.n_rows == 0:  # an empty shard contributes zeros to the all-reduce
+            out.zero_()
+            return
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_reduce_partials(_ptr(self.partials), self.n_parts, n_out,
                                                 _ptr(self.stage), _ptr(self.counter), _ptr(out),
@@ -260,11 +323,14 @@ class MUPlan:
                 _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
                 _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
                 _ptr(self.AB), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H,
-                self.l2_H, int(apply_first), self._stream()), "cnmf_mu_shard_step")
+                self.l2_H, int(apply_first), self.layout, self._stream()), "cnmf_mu_shard_step")
 
     def _allreduce(self, t: torch.Tensor):
         if self.world > 1 or (self.shard_steps and self.group is not None):
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+            if getattr(self.group, "is_local", False):
+                self.group.all_reduce(t, "sum")
+            else:
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
     def check_sync_error(self):
         """Raise if a persistent launch gave up waiting for a workgroup (its results are invalid);
@@ -285,7 +351,7 @@ class MUPlan:
         """The persistent launch this plan's shape takes (kernel, layout, W residency, grid)."""
         buf = ctypes.create_string_buffer(256)
         with torch.cuda.device(self.device):
-            check(self.lib.cnmf_persist_describe(self.n_rows, self.F, self.k, self.xdt, buf, 256),
+            check(self.lib.cnmf_persist_describe(self.n_rows, self.F, self.k, self.xdt, self.layout, buf, 256),
                   "cnmf_persist_describe")
         return buf.value.decode()
 
@@ -303,12 +369,12 @@ class MUPlan:
             args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
                     _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AB),
                     self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl),
-                    *ev, self._stream())
+                    self.layout, *ev, self._stream())
         elif self.world == 1 and not self.shard_steps and self.persistent:
             fn, name = self.lib.cnmf_mu_iterations, "cnmf_mu_iterations"
             args = (n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
                     _ptr(self.partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self.AB), None,
-                    self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H, *ev,
+                    self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H, self.layout, *ev,
                     self._stream())
         else:
             return lambda: self.iterate(n_iter, pass_events=pass_events)
@@ -330,7 +396,7 @@ class MUPlan:
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
                     _ptr(self.counter), _ptr(self.AB), self.n_rows, self.F, self.k,
-                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl),
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, _ptr(self.xctl), self.layout,
                     *_event_array(pass_events), self._stream()), "cnmf_mu_iterations_multi")
             return
         if self.world == 1 and not self.shard_steps and self.persistent_shape and not self.persistent:
@@ -346,7 +412,7 @@ class MUPlan:
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),
                     _ptr(self.HHt), _ptr(self.partials), self.n_parts, _ptr(self.stage),
                     _ptr(self.counter), _ptr(self.AB), None, self.n_rows, self.F, self.k,
-                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, *_event_array(pass_events),
+                    self.l1_W, self.l2_W, self.l1_H, self.l2_H, self.layout, *_event_array(pass_events),
                     self._stream()), "cnmf_mu_iterations")
             return
         # multi-GPU: per iteration ONE shard step (pending basis update from the all-reduced AB,
@@ -363,36 +429,46 @@ class MUPlan:
         self.basis_update()
 
     def tune(self, n_iter: int = 100, rounds: int = 2, variants=(4, 1, 2)) -> dict:
-        """Time the layouts of the persistent launch (cnmf_set_persist_variant: 4 = wave tiles,
-        1 = pairs of 4-wave workgroups, 2 = 8-wave two-team workgroups; 3 = pairs with floating
-        tiles is not bit-repeatable and only timed when asked for) on this plan's shape and keep
-        the fastest for the process.  Runs on copies of W and H: the plan's state is unchanged.
-        Call after the GPU has been busy for a while (the clock ramps up over the first ~35 ms of
-        work).  Returns {variant: mean µs per iteration}.  No-op (empty dict) for non-persistent
-        plans."""
+        """Time the layouts of the persistent launch (the `layout` argument, include/cnmf_hip.h:
+        4 = wave tiles, 1 = pairs of 4-wave workgroups, 2 = 8-wave two-team workgroups; 3 = pairs
+        with floating tiles is not bit-repeatable and only timed when asked for) on this plan's
+        shape and keep the fastest for THIS plan.  Runs on copies of W and H: the plan's state is
+        unchanged.  Collective over the plan's group: every rank times the same launches in the
+        same order, the per-layout times are max-reduced over the ranks and every rank keeps the
+        same layout (the ranks' launches must match: the in-launch exchange, and the shard steps'
+        partial sums).  Call after the GPU has been busy for a while (the clock ramps up over the
+        first ~35 ms of work).  Returns {layout: µs per iteration, the slowest rank's}.  No-op
+        (empty dict) for non-persistent plans."""
         if not self.persistent or self.k != 4 or self.xdt != _lib.F32:
             return {}  # the layouts are alternatives for fp32 k = 4 only (k = 8: wave tiles)
         W0, H0 = self.W.clone(), self.H64.clone()
-        stream = torch.cuda.current_stream(self.device)
+        keep = self.layout
         times = {v: [] for v in variants}
         try:
             for _ in range(rounds):
                 for v in variants:
-                    check(self.lib.cnmf_set_persist_variant(v), "cnmf_set_persist_variant")
-                    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-                    ev[0].record(stream)
-                    self.iterate(n_iter)
-                    ev[1].record(stream)
-                    torch.cuda.synchronize(self.device)
-                    self.check_sync_error()
-                    times[v].append(ev[0].elapsed_time(ev[1]) * 1e3 / n_iter)
+                    self.layout = v
+                    times[v].append(self._time_iterations(n_iter) * 1e6 / n_iter)
         finally:
             self.W.copy_(W0)
             self.H64.copy_(H0)
             self.refresh_basis()
-        best = min(times, key=lambda v: sum(times[v]))
-        check(self.lib.cnmf_set_persist_variant(best), "cnmf_set_persist_variant")
-        return {v: sum(t) / len(t) for v, t in times.items()}
+            self.layout = keep
+        mean = [sum(times[v]) / len(times[v]) for v in variants]
+        mean = dict(zip(variants, agree_max(mean, self.group if self.world > 1 else None, self.device)))
+        self.layout = min(variants, key=lambda v: (mean[v], variants.index(v)))
+        return mean
+
+    def _time_iterations(self, n_iter: int) -> float:
+        """Seconds of one n_iter launch on the plan's stream (HIP events); raises on a failed launch."""
+        stream = torch.cuda.current_stream(self.device)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record(stream)
+        self.iterate(n_iter)
+        ev[1].record(stream)
+        torch.cuda.synchronize(self.device)
+        self.check_sync_error()
+        return ev[0].elapsed_time(ev[1]) / 1e3
 
     _NORMS = {"l1": 1, "l2": 2, "max": 3}
 
@@ -423,22 +499,39 @@ class MUPlan:
         return self.H64.to(dtype or self.tc)
 
 
-def _iterate_guarded(plan, n_iter: int, update_H: bool):
-    """plan.iterate(n_iter) for a persistent plan, with a way back: W and H are snapshotted before
-    the launch; if it reports a synchronisation failure (a workgroup never co-resident, a peer rank
-    timed out: HipLibraryError from check_sync_error, results invalid), the snapshot is restored and
-    the stretch re-run on the per-iteration path (single GPU) or the RCCL path (multi-GPU; every
-    rank fails the same launch, the exchange poisons its peers).  Synchronises."""
+def sync_failed(plan) -> bool:
+    """check_sync_error() as a collective verdict: True on EVERY rank of the plan's group when the
+    last launch failed on ANY rank (a rank deciding the fallback from its own error word
+    alone re-runs a stretch its peers do not, and the collectives stop matching).  Synchronises."""
     import warnings
-    W0, H0 = plan.W.clone(), plan.H64.clone()
-    plan.iterate(n_iter, update_H)
+    failed = False
     try:
         plan.check_sync_error()
     except _lib.HipLibraryError as e:
+        failed = True
         warnings.warn(f"{e}; the stretch is re-run on the per-iteration path", RuntimeWarning)
+    if plan.world > 1:
+        failed = agree_max([1.0 if failed else 0.0], plan.group, plan.device)[0] != 0.0
+    return failed
+
+
+def _iterate_guarded(plan, n_iter: int, update_H: bool):
+    """plan.iterate(n_iter) for a persistent plan, with a way back: W and H are snapshotted before
+    the launch; if it reports a synchronisation failure on any rank (a workgroup never co-resident,
+    a peer rank timed out: results invalid), EVERY rank restores its snapshot and re-runs the
+    stretch on the per-iteration path (single GPU) or the RCCL path (multi-GPU).  Synchronises."""
+    import warnings
+    W0, H0 = plan.W.clone(), plan.H64.clone()
+    plan.iterate(n_iter, update_H)
+    if sync_failed(plan):
+        if plan.world > 1:
+            warnings.warn("a rank's persistent launch failed: every rank re-runs the stretch on the "
+                          "RCCL path", RuntimeWarning)
         plan.W.copy_(W0)
         plan.H64.copy_(H0)
         plan.refresh_basis()
+        if getattr(plan, "exchange", False):
+            plan.disable_exchange()
         plan.exchange = False
         plan.persistent = False
         plan.iterate(n_iter, update_H)
@@ -509,6 +602,8 @@ class ALSPlan(MUPlan):
                                             self._stream()), "cnmf_als_prepare")
 
     def w_step(self, accumulate: bool = True):
+        if self.n_rows == 0:  # an empty shard (world > rows): reduce() then contributes zeros
+            return
         with torch.cuda.device(self.device):
             check(self.lib.cnmf_als_sample_pass(
                 _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.Ht), _ptr(self.table),
@@ -658,7 +753,10 @@ class WeightedMUPlan:
 
     def _allreduce(self, t: torch.Tensor):
         if self.world > 1:
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+            if getattr(self.group, "is_local", False):
+                self.group.all_reduce(t, "sum")
+            else:
+                torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
 
     def refresh_basis(self):
         pass  # the weighted kernels read H64 itself
@@ -733,6 +831,7 @@ class WeightedMUPlan:
     # the in-launch cross-rank exchange (MUPlan's: IPC-shared buffers, cnmf_xctl_init), for the
     # persistent weighted launch; collective over the plan's group
     enable_exchange = MUPlan.enable_exchange
+    _enable_exchange_local = MUPlan._enable_exchange_local
     disable_exchange = MUPlan.disable_exchange
     release = MUPlan.release
     _pci_bus_id = MUPlan._pci_bus_id

@@ -20,7 +20,8 @@
  * the one-off occupancy query); every launch is asynchronous on `stream` (a hipStream_t, NULL = the
  * default stream); entry points return 0 or a negative cnmf_status and set a thread-local
  * message readable with cnmf_last_error().  Re-entrant; no global mutable state except that
- * message and a per-device occupancy cache.
+ * message and a per-device occupancy cache; the environment is not read (the diagnostic build,
+ * -DCNMF_DIAG, adds A/B switches and a bandwidth probe, and is never loaded by the product).
  */
 #ifndef CNMF_HIP_H
 #define CNMF_HIP_H
@@ -100,25 +101,22 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
 int64_t cnmf_counter_words(void);
 int cnmf_counter_err_word(void);
 
-/* 1 when cnmf_mu_iterations runs this shape as ONE persistent launch (mu_iter_sl_kernel: fp32 X,
- * F = 81, k = 4, n_rows a multiple of 64 and >= 192), 0 when it launches pass + reduce per
+/* 1 when cnmf_mu_iterations runs this shape as ONE persistent launch (fp32 X, F = 81, k = 4 or 8,
+ * n_rows a multiple of 64 / k with enough tiles per wave), 0 when it launches pass + reduce per
  * iteration. */
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
 
-/* Process-wide layout of persistent launches (results agree to fp32 rounding of the partial sums,
- * not bit for bit): 4 = wave tiles (default): one 4-wave workgroup per CU, each wave streaming its
- * own 16-sample tiles with no barrier inside an iteration, W resident in LDS (CNMF_WT_PD = 2..4
- * tiles in flight per wave, default 3); 1 = two independent 4-wave workgroups per CU on 64-sample
- * tiles, 2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart,
- * 3 = layout 1 with floating tiles: a fraction `frac` of the tiles stays with its workgroup (W
- * resident), the rest is drawn from a pool every iteration so that faster CUs take more (not
- * bit-repeatable: the draw decides the summation order).  MUPlan.tune() times 4, 1 and 2 and keeps
- * the fastest.  cnmf_set_persist_dyn_frac: frac in (0, 1] (default 0.8, env CNMF_DYN_FRAC); a shape
- * with fewer than 4 static tiles per workgroup uses layout 1, one whose W does not fit LDS under
- * layout 4 uses layout 1. */
-int cnmf_set_persist_variant(int variant);
-int cnmf_get_persist_variant(void);
-int cnmf_set_persist_dyn_frac(double frac);
+/* `layout` of a persistent launch (an argument of every call that launches one; a plan keeps its
+ * own: nothing is process-wide).  Results agree to fp32 rounding of the partial sums, not bit for bit:
+ *   0 = default (4);
+ *   4 = wave tiles: one 4-wave workgroup per CU, each wave streaming its own 16-sample (k = 4) or
+ *       8-sample (k = 8) tiles with no barrier inside an iteration, W resident in LDS when it fits;
+ *   1 = two independent 4-wave workgroups per CU on 64-sample tiles (k = 4);
+ *   2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart (k = 4);
+ *   3 = layout 1 with floating tiles: 80 % of the tiles stay with their workgroup (W resident), the
+ *       rest is drawn from a pool every iteration (not bit-repeatable: the draw decides the order).
+ * MUPlan.tune() times 4, 1 and 2 and keeps the fastest for its plan.  k = 8 has layout 4 only;
+ * other values are CNMF_ERR_ARG. */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
  * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction
@@ -131,7 +129,7 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,
                        int n_features, int k, double l1_W, double l2_W, double l1_H, double l2_H,
-                       void* const* events, int n_events, void* stream);
+                       int layout, void* const* events, int n_events, void* stream);
 
 /* One MU iteration of a row shard for the multi-GPU driver (SK:831-870 with the accumulators
  * all-reduced between ranks):
@@ -143,7 +141,7 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
 int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
                        double* partials, int64_t n_parts, double* stage, uint32_t* counter, double* AB,
                        int64_t n_rows, int n_features, int k, double l1_W, double l2_W, double l1_H,
-                       double l2_H, int apply_first, void* stream);
+                       double l2_H, int apply_first, int layout, void* stream);
 
 /* ---- Multi-GPU with the all-reduce inside the persistent launch (persistent shapes only).
  * Each rank allocates one exchange buffer (fine-grained device memory, zeroed) and exports its IPC
@@ -161,13 +159,22 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
  * cnmf_mu_shard_step + an RCCL all-reduce). */
 /* The persistent launch cnmf_mu_iterations would use for this shape, as text (kernel, layout,
  * W residency, grid) into out[len]; returns 1 (persistent), 0 (per-iteration launches) or < 0. */
-int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, char* out, int len);
+int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, int layout, char* out,
+                          int len);
 int64_t cnmf_xbuf_bytes(int world);
 int cnmf_xbuf_handle_bytes(void);
 /* Peer checks before the exchange: the PCI bus id of a visible device ("dddd:bb:dd.f", len >= 16)
  * and whether `device` can map `peer`'s memory (1 / 0). */
 int cnmf_device_pci_bus_id(int device, char* out, int len);
 int cnmf_device_can_access_peer(int device, int peer);
+/* Map `peer`'s memory into `device`'s kernels (hipDeviceEnablePeerAccess with `device` current;
+ * idempotent; the current device is restored) — several devices driven from ONE process
+ * (cnmf_amd.multidevice) exchange through directly mapped buffers, no IPC. */
+int cnmf_enable_peer_access(int device, int peer);
+/* Workgroups of the persistent launch for this shape and layout (multi: the in-launch exchange
+ * form), 0 when the shape runs per-iteration launches; every one is resident for the whole launch
+ * (one per CU for the wave tiles), so co-running launches on one device must fit together. */
+int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int layout, int multi);
 int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle);
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr);
 int cnmf_xbuf_close(void* dptr);
@@ -178,7 +185,7 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
                              double* Ht, double* HHt, double* partials, int64_t n_parts,
                              double* stage, uint32_t* counter, double* AB, int64_t n_rows,
                              int n_features, int k, double l1_W, double l2_W, double l1_H,
-                             double l2_H, uint64_t* xctl, void* const* events, int n_events,
+                             double l2_H, uint64_t* xctl, int layout, void* const* events, int n_events,
                              void* stream);
 
 /* Normalisation projection (no sklearn counterpart, off unless asked for):
@@ -234,9 +241,6 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
                               double sum_to_one, double smoothness, uint64_t* xctl, void* const* events,
                               int n_events, void* stream);
 
-/* Diagnostic: stream-read `bytes` of `buf` (16-byte loads, n_blocks x 256 threads) writing one
- * checksum per block to out[n_blocks]; times the achievable HBM read ceiling for DESIGN.md. */
-int cnmf_hbm_probe(const void* buf, int64_t bytes, double* out, int n_blocks, void* stream);
 
 /* ---- weighted / masked MU (oracle/wmu_ref.py).  Per-element weights
  * M >= 0 (N x F fp32, same layout as X; 0 = missing):

@@ -30,6 +30,17 @@ def test_error_paths_return_status():
     assert lib.cnmf_pass_blocks(100, 81, 4, 9) == -1   # unknown dtype
     with pytest.raises(_lib.HipLibraryError):
         _lib.check(-3, "probe")
+    # a bad layout is refused before anything touches a device
+    assert lib.cnmf_persist_describe(1024, 81, 4, 0, 7, b"\0" * 64, 64) == -1
+    assert b"layout" in lib.cnmf_last_error()
+
+
+def test_product_library_has_no_diagnostic_switches():
+    """VERDICT r2 #8: the probe and the process-wide layout setters live in the diagnostic build."""
+    lib = _lib.load()
+    for name in ("cnmf_hbm_probe", "cnmf_set_persist_variant", "cnmf_get_persist_variant",
+                 "cnmf_set_persist_dyn_frac"):
+        assert not hasattr(lib, name), name
 
 
 def test_prepared_calls_match_the_declared_signatures():
@@ -41,8 +52,9 @@ def test_prepared_calls_match_the_declared_signatures():
     lib = _lib.load()
     ev = ((ctypes.c_void_p * 2)(1, 2), 2)
     calls = {
-        "cnmf_mu_iterations": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, None, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, *ev, 0),
-        "cnmf_mu_iterations_multi": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, 1, *ev, 0),
+        "cnmf_mu_iterations": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, None, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, 0, *ev, 0),
+        "cnmf_mu_iterations_multi": (20, 1, 0, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 0.0, 0.0, 0.0, 0.0, 1, 0, *ev,
+                                     0),
         "cnmf_als_iterations": (20, 1, 0, 1, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 1.0, 0.5, *ev, 0),
         "cnmf_als_iterations_multi": (20, 1, 0, 1, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, 1.0, 0.5, 1, *ev, 0),
         "cnmf_wmu_iterations": (20, 1, 1, 1, 1, 1, 8, 1, 1, 1, 1024, 81, 4, *ev, 0),

@@ -214,3 +214,99 @@ def test_two_rank_gloo_weighted_matches_unsharded(tol, max_iter):
         assert n_iter == nr
         np.testing.assert_allclose(Hp, Hr, rtol=1e-10, atol=1e-14)
     np.testing.assert_allclose(W, Wr, rtol=1e-10, atol=1e-14)
+
+
+class _FlakyExchangePlan(_NumpyPlan):
+    """A multi-GPU plan on the persistent in-launch-exchange path whose FIRST launch fails on rank 0
+    only: its error word is set and its results are invalid (W scaled), while rank 1's
+    launch completed with valid results.  The in-launch exchange is modelled by one all_reduce per
+    iteration, so the collectives of both ranks stay paired however the fallback goes."""
+
+    def __init__(self, *a, rank=0, **kw):
+        super().__init__(*a, **kw)
+        self.rank = rank
+        self.persistent = self.persistent_shape = self.exchange = True
+        self.device = torch.device("cpu")
+        self._fail_next = rank == 0
+        self._err = False
+        self.W = torch.zeros(1)  # snapshot targets of _iterate_guarded (mirrors Wn / Hn below)
+        self.H64 = torch.zeros(1)
+        self.fallbacks = 0
+
+    def iterate(self, n_iter, update_H=True, pass_events=None):
+        if not self.exchange:
+            self.fallbacks += 1
+        for i in range(n_iter):
+            self.shard_step(apply_first=i > 0)
+            self._allreduce(self.AB)
+        self.basis_update()
+        if self.exchange and self._fail_next:
+            self._fail_next, self._err = False, True
+            self.Wn = self.Wn * 2.0  # the failed launch's results are invalid
+
+    def check_sync_error(self):
+        if self._err:
+            self._err = False
+            self.disable_exchange()
+            raise _lib.HipLibraryError("multi-GPU persistent launch failed (forced on one rank)")
+
+    def _allreduce(self, t):
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.group)
+
+    def disable_exchange(self):
+        self.exchange = False
+
+    def refresh_basis(self):
+        pass
+
+
+def _snapshotting(plan):
+    """Route _iterate_guarded's W / H64 snapshot and restore through the NumPy state."""
+    class _T:
+        def __init__(self, get, put):
+            self.get, self.put = get, put
+
+        def clone(self):
+            return self.get().copy()
+
+        def copy_(self, v):
+            self.put(v.copy())
+    plan.W = _T(lambda: plan.Wn, lambda v: setattr(plan, "Wn", v))
+    plan.H64 = _T(lambda: plan.Hn, lambda v: setattr(plan, "Hn", v))
+    return plan
+
+
+def _flaky_worker(rank, world, port, X, W0, H0, out):
+    import warnings
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = shard_bounds(X.shape[0], world, rank)
+        plan = _snapshotting(_FlakyExchangePlan(X[lo:hi], W0[lo:hi], H0, group=dist.group.WORLD, rank=rank))
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            n_iter = run_mu(plan, max_iter=30, tol=1e-3)
+        out[rank] = (lo, hi, plan.Wn, plan.Hn, n_iter, plan.fallbacks, plan.exchange)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_failed_launch_on_one_rank_falls_back_on_every_rank():
+    """a persistent multi-GPU launch that fails on ONE rank makes EVERY rank
+    restore its snapshot and re-run the stretch on the RCCL path (a collective verdict): both ranks
+    end on the unsharded oracle's factors with identical H and the same n_iter."""
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(257, 81, seed=21, dtype=np.float64)
+    W0, H0 = random_init(X, 4, 9)
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_flaky_worker, args=(2, _free_port(), X, W0, H0, out), nprocs=2, join=True)
+    Wr, Hr, nr = mu_ref.mu_fit(X, W0, H0, max_iter=30, tol=1e-3)
+    W = np.zeros_like(W0)
+    for rank in range(2):
+        lo, hi, Wp, Hp, n_iter, fallbacks, exchange = out[rank]
+        W[lo:hi] = Wp
+        assert n_iter == nr and fallbacks >= 1 and not exchange
+        np.testing.assert_allclose(Hp, Hr, rtol=1e-10, atol=1e-14)
+    np.testing.assert_array_equal(out[0][3], out[1][3])
+    np.testing.assert_allclose(W, Wr, rtol=1e-10, atol=1e-14)

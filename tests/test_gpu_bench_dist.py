@@ -1,0 +1,74 @@
+"""bench.py at N = 2 on ONE GPU: two ranks launched as the driver launches them
+(RANK / WORLD_SIZE / MASTER_* in the environment), sharing cuda:0 over the gloo backend (RCCL needs
+distinct devices; the kernels, the in-launch exchange through IPC and every collective decision
+of the bench are the same).  The run must finish, validate the in-launch exchange against the
+host-collective path, time it, and report the same layout on both ranks.
+
+The problem is small enough (32768 rows: 64 workgroups per rank) that both ranks' persistent grids
+are co-resident on the one GPU, as the exchange requires.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_two_ranks(extra, timeout=240):
+    port = _free_port()
+    procs = []
+    for rank in range(2):
+        env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
+                   LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+               "--steps", "20", "--warmup", "20", "--no-cpu", "--ramp-seconds", "0.2"] + extra
+        procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            outs.append((p.returncode, o, e))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for rc, o, e in outs:
+        assert rc == 0, e[-3000:]
+    lines = [ln for ln in outs[0][1].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[0][1][-2000:]
+    assert not [ln for ln in outs[1][1].splitlines() if ln.startswith("{")]  # rank 0 prints alone
+    return json.loads(lines[0]), outs
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_one_gpu_exchange():
+    res, outs = _run_two_ranks(["--rows", "32768"])
+    cfg = res["config"]
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert cfg["exchange"].startswith("validated"), cfg["exchange"]
+    lay = cfg["layout_per_rank"]
+    assert len(lay) == 2 and lay[0] == lay[1]
+    assert cfg["clock_ramp_trips"] >= 1
+    assert res["roofline"]["iterations_per_launch"] == 20  # the 20 steps as ONE launch per rank
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_one_gpu_host_collective_path():
+    """--exchange off: one shard step + one all_reduce per iteration on both ranks."""
+    res, _ = _run_two_ranks(["--rows", "32768", "--exchange", "off", "--no-tune"])
+    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["config"]["exchange"] is None
+    assert res["roofline"]["launches_timed"] == 20

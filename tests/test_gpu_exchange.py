@@ -37,10 +37,11 @@ def _data(N, seed, k=4):
     return X, W0, H0
 
 
-def _plan(X, W0, H0, group=None):
+def _plan(X, W0, H0, group=None, layout=0):
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1], group=group)
+    plan.layout = layout
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
@@ -50,12 +51,7 @@ def _plan(X, W0, H0, group=None):
 def layout(request):
     """Every persistent layout a rank may pick (MUPlan.tune runs them all at N > 1 too); the
     multi-GPU launch serves layout 3 with layout 1 (floating tiles are single-GPU only)."""
-    from cnmf_amd import _lib
-    lib = _lib.load()
-    old = lib.cnmf_get_persist_variant()
-    assert lib.cnmf_set_persist_variant(request.param) == 0
-    yield request.param
-    lib.cnmf_set_persist_variant(old)
+    return request.param
 
 
 def test_self_exchange_is_bit_identical(layout):
@@ -63,17 +59,14 @@ def test_self_exchange_is_bit_identical(layout):
     import torch.distributed as dist
     from cnmf_amd import _lib
     X, W0, H0 = _data(64 * 1500, 5)
-    lib = _lib.load()
-    if layout == 3:  # the multi launch runs layout 1: compare with the single-GPU layout 1
-        lib.cnmf_set_persist_variant(1)
-    ref = _plan(X, W0, H0)
+    # the multi launch runs layout 3 as layout 1: compare with the single-GPU layout 1
+    ref = _plan(X, W0, H0, layout=1 if layout == 3 else layout)
     assert ref.persistent
     ref.iterate(25)
     ref.check_sync_error()
-    lib.cnmf_set_persist_variant(layout)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
     try:
-        plan = _plan(X, W0, H0, group=dist.group.WORLD)
+        plan = _plan(X, W0, H0, group=dist.group.WORLD, layout=layout)
         plan.enable_exchange()
         assert plan.exchange and plan.persistent
         plan.iterate(10)

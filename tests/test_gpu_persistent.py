@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 TOL32 = 1e-5
 
 
-def _plan(X, W0, H0, **regs):
+def _plan(X, W0, H0, layout=0, **regs):
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1], **regs)
+    plan.layout = layout
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
@@ -37,16 +38,11 @@ def _unfused(plan, n):
 
 @pytest.fixture(params=[4, 1, 2, 3], ids=["wave", "pairs", "teams", "floating"])
 def layout(request):
-    """The persistent launch's layouts (cnmf_set_persist_variant): pairs of 4-wave workgroups per
-    CU, one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart), or pairs with
-    floating tiles (a pool drawn every iteration; shapes with < 4 static tiles per workgroup fall
-    back to pairs)."""
-    from cnmf_amd import _lib
-    lib = _lib.load()
-    old = lib.cnmf_get_persist_variant()
-    assert lib.cnmf_set_persist_variant(request.param) == 0
-    yield request.param
-    lib.cnmf_set_persist_variant(old)
+    """The persistent launch's layouts (the plan's `layout` argument): wave tiles, pairs of 4-wave
+    workgroups per CU, one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart), or
+    pairs with floating tiles (a pool drawn every iteration; shapes with < 4 static tiles per
+    workgroup fall back to pairs)."""
+    return request.param
 
 
 # 40 / 1000 / 4096 tiles: few tiles per (virtual) workgroup, a padding step for one of the teams
@@ -57,7 +53,7 @@ def test_persistent_matches_oracle(n_tiles, layout):
     N = 64 * n_tiles
     X = iop_spectra(N, 81, seed=n_tiles, dtype=np.float32)
     W0, H0 = random_init(X, 4, 42)
-    plan = _plan(X, W0, H0)
+    plan = _plan(X, W0, H0, layout)
     assert plan.persistent, "shape should take the persistent launch"
     n_it = 200 if n_tiles < 15625 else 40  # the full cfg2 size: a shorter oracle run
     plan.iterate(n_it)
@@ -78,26 +74,21 @@ def test_layouts_agree_and_are_deterministic():
     """The two layouts group the per-workgroup fp32 partial sums differently: agreement to fp32
     summation-order noise; each is bit-for-bit repeatable, also across split launches."""
     import torch
-    from cnmf_amd import _lib
     from cnmf_amd.synthetic import iop_spectra, random_init
-    lib = _lib.load()
-    old = lib.cnmf_get_persist_variant()
     X = iop_spectra(64 * 3001, 81, seed=21, dtype=np.float32)
     W0, H0 = random_init(X, 4, 5)
     out = {}
-    try:
-        for v in (4, 1, 2):
-            lib.cnmf_set_persist_variant(v)
-            a, c = _plan(X, W0, H0), _plan(X, W0, H0)
-            a.iterate(60)
-            for n in (7, 23, 30):
-                c.iterate(n)
-            a.check_sync_error()
-            c.check_sync_error()
-            assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
-            out[v] = (a.W.cpu().numpy(), a.H64.cpu().numpy())
-    finally:
-        lib.cnmf_set_persist_variant(old)
+    for v in (4, 1, 2):
+        a, c = _plan(X, W0, H0, v), _plan(X, W0, H0, v)
+        a.iterate(60)
+        for n in (7, 23, 30):
+            c.iterate(n)
+        a.check_sync_error()
+        c.check_sync_error()
+        assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
+        out[v] = (a.W.cpu().numpy(), a.H64.cpu().numpy())
+    # a plan's layout is its own: two plans with different layouts side by side
+    assert "wt_kernel" in _plan(X, W0, H0, 4).describe() and "sl_kernel" in _plan(X, W0, H0, 1).describe()
     for v in (2, 4):
         assert rel_fro(out[1][0], out[v][0]) < 1e-6 and rel_fro(out[1][1], out[v][1]) < 1e-6
 
@@ -149,44 +140,33 @@ def test_persistent_tol_stop_through_api():
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32
 
 
-# (tiles, frac): no floating tile at all (every workgroup's one draw fails), the minimum of 4 static
-# tiles with half the tiles floating, cfg2's tile count at the default fraction, a ragged count
-@pytest.mark.parametrize("n_tiles,frac", [(4096, 1.0), (4096, 0.5), (15625, 0.8), (3001, 0.7)])
-def test_floating_tiles(n_tiles, frac):
+# the product's resident fraction is 0.8 (CNMF_DYN_FRAC varies it in the diagnostic build only):
+# cfg2's tile count, a count with the minimum static tiles, a ragged count
+@pytest.mark.parametrize("n_tiles", [4096, 15625, 3001])
+def test_floating_tiles(n_tiles):
     """Layout 3: tiles drawn from a pool every iteration, their W handed between workgroups (and
     XCDs) through HBM.  Every tile must be updated exactly once per iteration: the factors match the
     oracle and the static layout (to fp32 summation-order noise), across split launches too, and the
     counters (tickets and both pools) are back at rest."""
-    from cnmf_amd import _lib
     from cnmf_amd.synthetic import iop_spectra, random_init
-    lib = _lib.load()
-    old = lib.cnmf_get_persist_variant()
     X = iop_spectra(64 * n_tiles, 81, seed=n_tiles + 3, dtype=np.float32)
     W0, H0 = random_init(X, 4, 11)
     n_it = 60 if n_tiles < 15625 else 30
-    try:
-        assert lib.cnmf_set_persist_dyn_frac(frac) == 0
-        lib.cnmf_set_persist_variant(1)
-        ref = _plan(X, W0, H0)
-        ref.iterate(n_it)
-        lib.cnmf_set_persist_variant(3)
-        a, c = _plan(X, W0, H0), _plan(X, W0, H0)
-        a.iterate(n_it)
-        for n in (2, n_it // 2 - 2, n_it - n_it // 2):
-            c.iterate(n)
-        for p in (a, c):
-            p.check_sync_error()
-            assert p.counters_at_rest()
-    finally:
-        lib.cnmf_set_persist_dyn_frac(0.8)
-        lib.cnmf_set_persist_variant(old)
+    ref = _plan(X, W0, H0, 1)
+    ref.iterate(n_it)
+    a, c = _plan(X, W0, H0, 3), _plan(X, W0, H0, 3)
+    a.iterate(n_it)
+    for n in (2, n_it // 2 - 2, n_it - n_it // 2):
+        c.iterate(n)
+    for p in (a, c):
+        p.check_sync_error()
+        assert p.counters_at_rest()
     Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
                               max_iter=n_it, tol=0.0)
     for p in (a, c):
         W, H = p.W.cpu().numpy(), p.H64.cpu().numpy()
         assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
         assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6 and rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
-    assert lib.cnmf_set_persist_dyn_frac(0.0) != 0 and lib.cnmf_set_persist_dyn_frac(1.5) != 0
 
 
 

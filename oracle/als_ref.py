@@ -100,8 +100,12 @@ def frobenius_error(X, W, H):
     return float(np.sqrt(np.sum(R * R)))
 
 
-def als_fit(X, W, H, max_iter=100, tol=0.0, sum_to_one=0.0, smoothness=0.0, return_errors=False):
-    """The constrained-ALS driver (module docstring).  Returns (W, H, n_iter)."""
+def als_fit(X, W, H, max_iter=100, tol=0.0, sum_to_one=0.0, smoothness=0.0, return_errors=False,
+            w_step="nnls"):
+    """The constrained-ALS driver (module docstring).  Returns (W, H, n_iter).  w_step='enumerate'
+    solves the W-step with fcls_w_enumerate (the same minimisers as scipy's NNLS — pinned by
+    tests/test_als_oracle.py — vectorised over the samples, for oracle runs at 1e5 rows)."""
+    w_solve = fcls_w if w_step == "nnls" else fcls_w_enumerate
     X = np.asarray(X, dtype=np.float64)
     W = np.array(W, dtype=np.float64)
     H = np.array(H, dtype=np.float64)
@@ -112,7 +116,7 @@ def als_fit(X, W, H, max_iter=100, tol=0.0, sum_to_one=0.0, smoothness=0.0, retu
         errors.append((0, error_at_init))
     it = 0
     for it in range(1, max_iter + 1):
-        W = fcls_w(X, H, sum_to_one)
+        W = w_solve(X, H, sum_to_one)
         H = smooth_h_sweep(W.T @ X, W.T @ W, H, smoothness)
         if tol > 0 and it % 10 == 0:
             error = frobenius_error(X, W, H)

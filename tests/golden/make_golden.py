@@ -127,6 +127,41 @@ def main_init(manifest):
         print(f"{name:24s} {str(X.shape):14s} {str(X.dtype):8s} init={kw['init']}")
 
 
+def tall_cases():
+    """(name, seed, n_rows, kwargs): sklearn's DEFAULT fit (init=None -> nndsvda over randomized_svd,
+    tol=1e-4, max_iter=200) on tall fp32 X — the path cnmf's API routes X of >= 65,536 rows through
+    (VERDICT r2).  X is NOT stored: the test regenerates it from iop_spectra(seed) and checks its
+    sha256; only sklearn's start (_initialize_nmf) and result are stored."""
+    return [("tall_default_float32", 13, 65536, dict(n_components=4, random_state=0)),
+            # the same default start with a tolerance that stops early (n_iter semantics, SK:872-884)
+            ("tall_default_tol_float32", 14, 65536, dict(n_components=4, random_state=0, tol=1e-3,
+                                                         max_iter=500))]
+
+
+def main_tall(manifest):
+    from sklearn.decomposition import non_negative_factorization
+    from sklearn.decomposition._nmf import _initialize_nmf
+    manifest["tall_cases"] = {}
+    for name, seed, n, kw in tall_cases():
+        X = iop_spectra(n, 81, seed=seed, dtype=np.float32)
+        W0, H0 = _initialize_nmf(X, kw["n_components"], init=None, random_state=kw["random_state"])
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            W, H, n_iter = non_negative_factorization(X, solver="mu", **kw)
+        x_sha = hashlib.sha256(np.ascontiguousarray(X).tobytes()).hexdigest()
+        arrays = {"W_init": W0, "H_init": H0, "W": W, "H": H, "n_iter": np.int64(n_iter),
+                  "seed": np.int64(seed), "n_rows": np.int64(n), "x_sha256": np.array(x_sha),
+                  "kwargs": np.array(json.dumps(kw))}
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **arrays)
+        with open(path, "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+        manifest["tall_cases"][name] = {"sha256": digest, "kwargs": kw, "n_iter": int(n_iter),
+                                        "seed": seed, "shape": [n, 81], "dtype": "float32",
+                                        "x_sha256": x_sha}
+        print(f"{name:24s} {(n, 81)} float32 default init, n_iter={n_iter}")
+
+
 def main():
     from sklearn.decomposition import non_negative_factorization
     import sklearn
@@ -155,9 +190,22 @@ def main():
                                    "shape": list(X.shape), "dtype": str(X.dtype)}
         print(f"{name:24s} {str(X.shape):14s} {str(X.dtype):8s} n_iter={n_iter}")
     main_init(manifest)
+    main_tall(manifest)
+    with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+
+
+def main_only_tall():
+    """Add / refresh the tall default-init cases without rewriting the others."""
+    with open(os.path.join(HERE, "MANIFEST.json")) as f:
+        manifest = json.load(f)
+    main_tall(manifest)
     with open(os.path.join(HERE, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main()
+    if "--only-tall" in sys.argv:
+        main_only_tall()
+    else:
+        main()

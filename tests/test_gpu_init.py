@@ -53,18 +53,30 @@ def test_gpu_init_large_matches_host():
     assert ew <= 1e-5 and eh <= 1e-5, (ew, eh)
 
 
-def test_api_routes_tall_x_to_gpu_init():
-    """NMF(init=None) on X with >= GPU_INIT_MIN_ROWS rows: W0 comes from the GPU init (a device
-    tensor) and agrees with the host restatement; the fit that follows still runs."""
+def test_api_routes_tall_x_by_init_device():
+    """init=None on X with >= GPU_INIT_MIN_ROWS rows: init_device='auto' keeps float32 X on the host
+    restatement (sklearn's start, bit for bit on the same BLAS) and sends float64 X to the GPU init;
+    init_device='gpu' sends float32 X to the GPU init too (its distance to sklearn's fp32 start is
+    reported by tests/test_gpu_tall_default.py); the fit that follows runs either way."""
     import torch
     from cnmf_amd import api
     from cnmf_amd.init import initialize_nmf
     from cnmf_amd.synthetic import iop_spectra
     X = iop_spectra(api.GPU_INIT_MIN_ROWS + 1000, 81, seed=6, dtype=np.float32)
     W, H = api._initial_factors(X, 4, None, 3, None, False, None)
-    assert isinstance(W, torch.Tensor) and W.is_cuda
+    assert isinstance(W, np.ndarray)  # auto + float32: the host restatement
+    Wh32, Hh32 = initialize_nmf(X, 4, init=None, random_state=3)
+    assert np.array_equal(W, Wh32) and np.array_equal(H, Hh32)
+    Wg, Hg = api._initial_factors(X, 4, None, 3, None, False, None, init_device="gpu")
+    assert isinstance(Wg, torch.Tensor) and Wg.is_cuda
     Wh, Hh = initialize_nmf(X.astype(np.float64), 4, init=None, random_state=3)  # see above: fp64
-    assert rel_fro(W.cpu().numpy(), Wh) <= 1e-5 and rel_fro(H, Hh) <= 1e-5
+    assert rel_fro(Wg.cpu().numpy(), Wh) <= 1e-5 and rel_fro(Hg, Hh) <= 1e-5
+    X64 = X.astype(np.float64)
+    W64, _ = api._initial_factors(X64, 4, None, 3, None, False, None)
+    assert isinstance(W64, torch.Tensor) and W64.is_cuda  # auto + float64: the GPU init
+    assert rel_fro(W64.cpu().numpy(), Wh) <= 1e-8
     import cnmf_amd
     W1, H1, n = cnmf_amd.factorise(X, n_components=4, random_state=3, max_iter=20, tol=0.0)
     assert n == 20 and W1.shape == (X.shape[0], 4) and np.all(W1 >= 0)
+    with pytest.raises(ValueError):
+        cnmf_amd.factorise(X, n_components=4, init_device="tpu")

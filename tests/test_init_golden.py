@@ -28,3 +28,22 @@ def test_init_goldens_cover_the_family():
     inits = {load_init(n)["kwargs"]["init"] for n in init_names()}
     dts = {str(load_init(n)["X"].dtype) for n in init_names()}
     assert {"nndsvd", "nndsvda", "nndsvdar", None} <= inits and dts == {"float32", "float64"}
+
+
+@pytest.mark.parametrize("name", ["tall_default_float32", "tall_default_tol_float32"])
+def test_tall_default_start_is_sklearns(name):
+    """The start cnmf's default fit takes for a tall float32 X (init_device='auto': the host
+    restatement) is sklearn's _initialize_nmf output bit for bit (X regenerated from its seed)."""
+    import hashlib
+    import json
+    import os
+    from cnmf_amd.init import initialize_nmf
+    from cnmf_amd.synthetic import iop_spectra
+    from golden_io import GOLDEN
+    z = np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False)
+    X = iop_spectra(int(z["n_rows"]), 81, seed=int(z["seed"]), dtype=np.float32)
+    assert hashlib.sha256(X.tobytes()).hexdigest() == str(z["x_sha256"])
+    kw = json.loads(str(z["kwargs"]))
+    W, H = initialize_nmf(X, kw["n_components"], init=None, random_state=kw["random_state"])
+    np.testing.assert_array_equal(W, z["W_init"])
+    np.testing.assert_array_equal(H, z["H_init"])

@@ -10,8 +10,9 @@ The hot loop runs in libcnmf_hip.so (hand-written HIP for gfx950, C ABI in inclu
 there is no CPU fallback.  See DESIGN.md.
 """
 from ._lib import HipLibraryError
+from ._trace import tracing
 from .api import NMF, ConvergenceWarning, factorise, fit, non_negative_factorization
 
 __version__ = "0.1.0"
 __all__ = ["factorise", "fit", "non_negative_factorization", "NMF", "ConvergenceWarning",
-           "HipLibraryError", "__version__"]
+           "HipLibraryError", "tracing", "__version__"]

@@ -84,6 +84,9 @@ _SIGS = {
     "cnmf_device_pci_bus_id": (_i32, [_i32, ctypes.c_char_p, _i32]),
     "cnmf_device_can_access_peer": (_i32, [_i32, _i32]),
     "cnmf_enable_peer_access": (_i32, [_i32, _i32]),
+    "cnmf_tolctl_doubles": (_i32, [_i32]),
+    "cnmf_mu_fit_tol": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _i32,
+                               _i32, _f64, _f64, _f64, _f64, _i32, _vp, _vp, _i32, _vp]),
     "cnmf_persist_workgroups": (_i64, [_i64, _i32, _i32, _i32, _i32, _i32]),
     "cnmf_xbuf_alloc": (_i32, [_i32, ctypes.POINTER(_vp), _vp]),
     "cnmf_xbuf_open": (_i32, [_vp, ctypes.POINTER(_vp)]),

@@ -2036,7 +2036,22 @@ struct PersistArgs {
   // (XC_* words, device memory), read only inside the exchange so that its values do not occupy
   // SGPRs through the streaming loop
   uint64_t* xctl;
+  // TOL (the tolerance test on the device, SK:872-884): the control block of TC_* doubles
+  double* tolctl;
 };
+
+// tolerance control block (doubles; TC_WSNAP holds a pointer's bits): inputs tol, it0 (global index
+// of the launch's first iteration), the capacity of the error list; in/out the error at init and the
+// previous checked error; outputs the iterations done, whether the test stopped the fit, whether
+// the stopped fit's W is in the snapshot buffer (streamed W) rather than in W itself, the count and
+// list of the checked errors (index g / 10 for the state after g iterations)
+constexpr int TC_TOL = 0, TC_IT0 = 1, TC_INIT = 2, TC_PREV = 3, TC_DONE = 4, TC_STOPPED = 5, TC_IN_SNAP = 6,
+              TC_WSNAP = 7, TC_CAP = 8, TC_NERR = 9, TC_ERRS = 16;
+static_assert(TC_TOL == CNMF_TC_TOL && TC_IT0 == CNMF_TC_IT0 && TC_INIT == CNMF_TC_INIT && TC_PREV == CNMF_TC_PREV &&
+                  TC_DONE == CNMF_TC_DONE && TC_STOPPED == CNMF_TC_STOPPED && TC_IN_SNAP == CNMF_TC_IN_SNAP &&
+                  TC_WSNAP == CNMF_TC_WSNAP && TC_CAP == CNMF_TC_CAP && TC_NERR == CNMF_TC_NERR && TC_ERRS == CNMF_TC_ERRS,
+              "tolerance control block slots = include/cnmf_hip.h");
+constexpr uint32_t FLAG_STOP = 1u << 30;  // the iteration flag of a launch the tolerance test stopped
 
 // exchange control block words: rank, world, byte offset of the flags in an exchange buffer, the
 // generation base (advanced by n_iter at the end of every launch, on the device), then the
@@ -2631,11 +2646,12 @@ struct Geo {
   static constexpr int L_WSTG = L_STG + NWV * XSTR;                     // streamed W: [NWV][WBW]
   static constexpr int L_RED = (L_WSTG + NWV * WBW + 15) / 16 * 16;     // [NWV][NL][NACC] fp32
   static constexpr int L_H = (L_RED + NWV * NL * NACC * 4 + 15) / 16 * 16;  // H fp64 [K][F]
-  static constexpr int L_AB = L_H + KK * F * 8;                         // AB fp64 [K][V]
-  static constexpr int L_HT = L_AB + NOUT * 8;                          // Hᵀ fp32 [NL·NQ][K]
+  static constexpr int L_AB = L_H + KK * F * 8;                         // AB fp64 [K][V] (+ the loss)
+  static constexpr int L_HT = L_AB + (NOUT + 2) * 8;                    // Hᵀ fp32 [NL·NQ][K]
   static constexpr int L_HHT = L_HT + NL * NQ * KK * 4;                 // HHᵀ fp64 [K][K]
-  static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 4 ints
-  static constexpr int L_WRES = (L_FLAG + 16 + 15) / 16 * 16;           // [NWV][nbt_max][WBW]
+  static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 8 ints
+  static constexpr int L_LOSS = L_FLAG + 32;                            // the waves' loss sums [NWV] fp64
+  static constexpr int L_WRES = (L_LOSS + 8 * NWV + 15) / 16 * 16;      // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
   static_assert(OVR >= 0 && PADB / 4 <= 64, "one zero float per lane covers the overrun");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
@@ -2898,11 +2914,20 @@ __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, doub
   wt_derive_basis<KK>(smem, t);
 }
 
-template <int KK, bool WRES, int PD, bool MULTI = false>
+// TOL: the tolerance test of SK:872-884 on the device.  In iteration g + 1 (g = it0 + it, g % 10 ==
+// 0) each lane also accumulates ‖x − w·H‖² of the state AFTER g iterations (x, the old w and H are
+// all in registers then: fp32 residual per element, fp64 sums per tile), carried as one more
+// column of the partial rows (NOUT + 1) and reduced / exchanged with [WᵀX | WᵀW]; the top combiner
+// applies the relative-decrease test.  On a stop it publishes the flag with FLAG_STOP and every
+// workgroup leaves with the state after g iterations: H (not updated), W as it was before this
+// iteration's update — written to W itself in the loss iterations when W is resident in LDS, else to
+// the snapshot buffer (TC_WSNAP; the host copies it) — so n_iter = g as in sklearn.
+template <int KK, bool WRES, int PD, bool MULTI = false, bool TOL = false>
 __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   using namespace wt;
   using G_ = Geo<KK>;
   constexpr int NL = G_::NL, TSW = G_::TSW, NQ = G_::NQ, V = G_::V, NOUT = G_::NOUT;
+  constexpr int NOUTT = NOUT + (TOL ? 1 : 0);  // partial-row width: + the loss of the checked state
   constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, NACC = G_::NACC;
   constexpr int PFW = G_::PFW, LASTL = G_::LASTL;
   constexpr int PFS = PFW + (WRES ? 0 : 1);  // loads per prefetch set (+ the W tile when streamed)
@@ -2930,6 +2955,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   double* sH = reinterpret_cast<double*>(smem + G_::L_H);
   double* sAB = reinterpret_cast<double*>(smem + G_::L_AB);
   int* sFlag = reinterpret_cast<int*>(smem + G_::L_FLAG);
+  double* sLoss = reinterpret_cast<double*>(smem + G_::L_LOSS);
+  // TOL: the launch's first global iteration, the snapshot buffer (streamed W)
+  const int it0 = TOL ? (int)ld_sc1(a.tolctl + TC_IT0) : 0;
+  float* wsnap = (TOL && !WRES)
+                     ? reinterpret_cast<float*>(__double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP)))
+                     : nullptr;
+  double lossacc = 0.0;  // this lane's ‖x − w·H‖² over the iteration's tiles (loss iterations)
   uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
   uint32_t* cnt_top = a.cnt + CNT_TOP;
   uint32_t* flag = a.cnt + CNT_FLAG;
@@ -3013,7 +3045,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // younger than it when its step waits (set q < PD: PD - q dummies, then the W stores of bodies
   // 0..q-1).  Counting PD stores that were never issued would let the set's last loads (the W tile)
   // still be in flight when it is staged.
-  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUT) + 64 * w + l;
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
@@ -3045,6 +3077,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       ++cur_it;
     }
     const bool last_it = it + 1 == a.n_iter;
+    const bool loss_it = TOL && ((it0 + it) % 10 == 0);  // check the state after it0 + it iterations
     const int64_t tile = gw + (int64_t)NW * i;
     // phase 1: x along the lane's row, packed fp32 chains of 7 features folded into fp64
     const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * e;
@@ -3124,7 +3157,28 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       wv[4 * m4 + 2] = v4.z;
       wv[4 * m4 + 3] = v4.w;
     }
-    const double wold = (double)wt_[s * KK + e];
+    const float wold32 = wt_[s * KK + e];
+    const double wold = (double)wold32;
+    if (loss_it) {
+      // ‖x − w·H‖² of the state before this update, the lane's NQ features (the last lane's overrun
+      // features past F belong to the next sample: masked)
+      float l2 = 0.f;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        f2 r2 = f2{0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < KP; ++q) r2 = __builtin_elementwise_fma(f2{wv[2 * q], wv[2 * q + 1]}, hp[c][q], r2);
+        const float r = NQ * e + c < F ? xv[c] - (r2.x + r2.y) : 0.f;
+        l2 = fmaf(r, r, l2);
+      }
+      lossacc += (double)l2;
+      // the W of that state: into W itself (resident W: HBM is not read again in this launch) or
+      // the snapshot buffer (streamed W).  Extra stores only make the counted waits stricter.
+      if (WRES)
+        reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wold32;
+      else
+        wsnap[(size_t)tile * TSW * KK + l] = wold32;
+    }
     double den = 0.0;
     if constexpr (KK == 8) {
       // den = w·HHᵀ[e] in packed fp32 (8 positive terms: no cancellation, ≤ 8 roundings), the
@@ -3181,10 +3235,18 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
     }
     zero_acc();
+    if (TOL) {  // the wave's loss sum (zero outside loss iterations), fixed xor tree
+      const double v = wave_sum(lossacc);
+      if (l == 0) sLoss[w] = v;
+      lossacc = 0.0;
+    }
     __syncthreads();
-    // the workgroup's fp64 row [K][V]: the four waves' sums in wave order (deterministic)
+    // the workgroup's fp64 row [K][V] (+ the loss): the four waves' sums in wave order (deterministic)
     {
-      double* prow = a.partials + (size_t)b * NOUT;
+      double* prow = a.partials + (size_t)b * NOUTT;
+      if (TOL && t == 0)
+        __hip_atomic_store(prow + NOUT, (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       for (int o = t; o < NOUT; o += NT) {
         const int j = o / V;
         const int v = o - j * V;
@@ -3204,10 +3266,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
       sFlag[1] = 0;
       sFlag[2] = 1;
+      sFlag[3] = 0;
     }
     __syncthreads();
+    // the last iteration of the launch waits for the flag too when it checks the tolerance (a stop
+    // there must reach every workgroup before it writes W back)
+    const bool must_wait = !last_it || loss_it;
     if (sFlag[0]) {  // group combiner
-      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -3216,16 +3282,82 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
-        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAB, a.AB, t);
-        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AB, sAB, err, it, t);
+        sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
+        if (TOL && loss_it && t == 0) {  // SK:872-884 on the state after it0 + it iterations
+          const int gi = it0 + it;
+          const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+          const int slot = gi / 10;
+          if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
+          st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
+          if (gi == 0) {
+            st_sc1(a.tolctl + TC_INIT, errv);
+            st_sc1(a.tolctl + TC_PREV, errv);
+          } else {
+            const double init = ld_sc1(a.tolctl + TC_INIT), prev = ld_sc1(a.tolctl + TC_PREV);
+            if ((prev - errv) / init < ld_sc1(a.tolctl + TC_TOL))
+              sFlag[3] = 1;
+            else
+              st_sc1(a.tolctl + TC_PREV, errv);
+          }
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0 && !last_it)
-          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == 0 && must_wait)
+          __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         TL_PUB(it);
       }
     }
     const bool top = sFlag[1] != 0;
+    if (!top && must_wait) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t f;
+        while (((f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~FLAG_STOP) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (TOL && (f & FLAG_STOP)) sFlag[3] = 1;
+      }
+      __syncthreads();
+      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
+        alive = false;
+        return;
+      }
+    }
+    if (TOL && sFlag[3]) {
+      // stopped by the tolerance test: the state after it0 + it iterations (W already where it
+      // belongs, H = sH not updated); the host clears the flag word after the launch
+      alive = false;
+      if (!top) return;
+      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < F * KK; o += NT) {
+        const int f = o / KK;
+        const int j = o - f * KK;
+        a.Ht[o] = sH[j * F + f];
+      }
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
+        st_sc1(a.tolctl + TC_STOPPED, 1.0);
+        st_sc1(a.tolctl + TC_IN_SNAP, WRES ? 0.0 : 1.0);
+        if (MULTI)
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
     if (last_it) {
       alive = false;
       if (WRES)  // this wave's W back to HBM, once per launch
@@ -3247,34 +3379,18 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!must_wait)  // (else workgroups may still poll it: the host clears it after the launch)
+          __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (TOL) {
+          st_sc1(a.tolctl + TC_DONE, (double)(it0 + a.n_iter));
+          st_sc1(a.tolctl + TC_STOPPED, 0.0);
+        }
         if (MULTI)  // the next launch's generations follow this one's
           __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
     if (!top) {
-      if (t == 0) {
-        const uint32_t want = (uint32_t)(it + 1);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-            sFlag[2] = 0;
-            break;
-          }
-          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
-            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sFlag[2] = 0;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      __syncthreads();
-      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
-        alive = false;
-        return;
-      }
       for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
     }
@@ -5978,17 +6094,20 @@ static int wt_pd(int k, bool wres, bool multi) {
 }
 extern "C++" {
 template <int KK, bool WRES>
-static PassFn wt_fn_k(int pd, bool multi) {
+static PassFn wt_fn_k(int pd, bool multi, bool tol) {
+  if (tol)  // the device tolerance test: PD = 3
+    return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true>)
+                 : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true>);
   if (multi) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true>);
   if (KK == 4 && WRES && pd == 2) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 2, false>);
   if (KK == 4 && WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 4, false>);
   return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false>);
 }
 }
-static PassFn wt_fn(int k, bool wres, bool multi) {
-  const int pd = wt_pd(k, wres, multi);
-  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi) : wt_fn_k<4, false>(pd, multi);
-  return wres ? wt_fn_k<8, true>(pd, multi) : wt_fn_k<8, false>(pd, multi);
+static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false) {
+  const int pd = tol ? 3 : wt_pd(k, wres, multi);
+  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol) : wt_fn_k<4, false>(pd, multi, tol);
+  return wres ? wt_fn_k<8, true>(pd, multi, tol) : wt_fn_k<8, false>(pd, multi, tol);
 }
 static int device_cus() {
   static int cus[64] = {0};
@@ -6004,7 +6123,8 @@ struct WtLaunch {
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
-static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, WtLaunch* out) {
+static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, WtLaunch* out,
+                    bool tol = false) {
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
   if (k == 4 && layout != 4) return false;
   const int tsw = 64 / k, wbw = tsw * k * 4;
@@ -6013,7 +6133,7 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
   const int ncu = device_cus();
   const int64_t n_tiles = n_rows / tsw;
   for (int wres = 1; wres >= 0; --wres) {
-    const int pd = wt_pd(k, wres != 0, multi);
+    const int pd = tol ? 3 : wt_pd(k, wres != 0, multi);
     // tiles per wave: > PD (the first prefetches), >= 2·PD + 1 when W is streamed (re-load hazard)
     const int min_nbt = wres ? pd + 1 : 2 * pd + 1;
     const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
@@ -6021,7 +6141,7 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
     if (lds > kMaxLds) continue;
-    const PassFn fn = wt_fn(k, wres != 0, multi);
+    const PassFn fn = wt_fn(k, wres != 0, multi, tol);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
     *out = WtLaunch{fn, G, n_tiles, lds};
     return true;
@@ -6153,7 +6273,8 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
 
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
                      double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
-                     double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl) {
+                     double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl,
+                     double* tolctl = nullptr) {
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
   PersistArgs pa;
@@ -6177,6 +6298,7 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
   pa.xctl = xctl;
+  pa.tolctl = tolctl;
   void* args[] = {&pa};
   HIP_CHECK(hipLaunchKernel(L.fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, s));
   return CNMF_OK;
@@ -6231,7 +6353,7 @@ int cnmf_counter_err_word(void) { return CNT_ERR; }
 // system-scope stores and loads over xGMI are coherent with this GPU's while both kernels run.
 constexpr int XBUF_MAX_WORLD = 64;
 static size_t xbuf_bytes(int world) {  // [2 parities][world][2·K·V] tagged 64-bit words
-  return (size_t)2 * world * 2 * wt::Geo<8>::NOUT * sizeof(uint64_t);  // the largest accumulator set
+  return (size_t)2 * world * 2 * (wt::Geo<8>::NOUT + 8) * sizeof(uint64_t);  // the largest accumulator set (+ loss)
 }
 
 int64_t cnmf_xbuf_bytes(int world) {
@@ -6357,6 +6479,7 @@ static int launch_persistent(int64_t G, int n_iter, const void* X, void* W, doub
   pa.apply_first = apply_first;
   pa.apply_last = apply_last;
   pa.xctl = xctl;
+  pa.tolctl = nullptr;
   const bool multi = xctl != nullptr;
   void* args[] = {&pa};
   if (n_iter > 1) {
@@ -6442,6 +6565,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
     pa.apply_first = apply_first;
     pa.apply_last = 0;
     pa.xctl = nullptr;
+    pa.tolctl = nullptr;
     void* args[] = {&pa};
     HIP_CHECK(hipLaunchKernel(persist_fn(), dim3((unsigned)G), dim3(NT), args, sl::L_PTOTAL, hs));
     return CNMF_OK;
@@ -6571,6 +6695,34 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
   return CNMF_OK;
 }
 
+
+int cnmf_tolctl_doubles(int max_iter) { return max_iter < 0 ? set_err(CNMF_ERR_ARG, "max_iter < 0") : TC_ERRS + max_iter / 10 + 1; }
+
+int cnmf_mu_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H64,
+                    double* Ht, double* HHt, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                    double* AB, double* tolctl, int64_t n_rows, int n_features, int k, double l1_W, double l2_W,
+                    double l1_H, double l2_H, int layout, uint64_t* xctl, void* const* events, int n_events,
+                    void* stream) {
+  hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+  RESOLVE_LAYOUT(layout);
+  if (max_iter <= 0) return set_err(CNMF_ERR_ARG, "max_iter must be >= 1");
+  WtLaunch L;
+  if (!wt_plan(n_rows, x_dtype, n_features, k, xctl != nullptr, layout, &L, true))
+    return set_err(CNMF_ERR_UNSUPPORTED, "the device tolerance test serves the wave-tile launch (fp32 X, F = 81, "
+                   "k = 4 or 8, layout 4; n_rows=%lld F=%d k=%d layout=%d)", (long long)n_rows, n_features, k, layout);
+  if (L.G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
+                                    (long long)n_parts, (long long)L.G);
+  if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !tolctl)
+    return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+  const int st = launch_wt(L, max_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
+                           0, 1, hs, xctl, tolctl);
+  if (st) return st;
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+  // the iteration flag may still hold the last (or the stopping) iteration: cleared in stream order
+  HIP_CHECK(hipMemsetAsync(counter + CNT_FLAG, 0, sizeof(uint32_t), hs));
+  return CNMF_OK;
+}
 
 // ---- weighted / masked MU
 int64_t cnmf_wmu_pass_blocks(int64_t n_rows, int n_features, int k) {

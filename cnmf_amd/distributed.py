@@ -41,7 +41,7 @@ def shard_bounds(n_rows: int, world: int, rank: int, align: int = 1):
 
 def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=0.0, l2_reg_W=0.0,
                       l1_reg_H=0.0, l2_reg_H=0.0, update_H=True, group=None, device=None,
-                      exchange=False, weights=None, solver="mu", sum_to_one=0.0, smoothness=0.0):
+                      exchange="auto", weights=None, solver="mu", sum_to_one=0.0, smoothness=0.0):
     """MU on this rank's rows; returns (W_shard, H, n_iter) as device tensors.
 
     X_shard: (n_r, F) float32/float64/bfloat16 tensor (any device; moved to `device`, default the
@@ -49,10 +49,13 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     here to make that true).  Regularisation constants are the already-scaled sklearn l1/l2 terms
     (SK:1254-1265 computed on the GLOBAL n_samples).
 
-    exchange=True: run each stretch of iterations as ONE persistent launch per rank with the
-    all-reduce inside the launch (peer exchange over xGMI, MUPlan.enable_exchange) when every
-    shard is a persistent shape (fp32, F = 81, k = 4, rows a multiple of 64); otherwise, or if the
-    buffers cannot be shared, a warning and the RCCL path.
+    exchange='auto' (default): run each stretch of iterations as ONE persistent launch per rank with
+    the all-reduce inside the launch (peer exchange over xGMI, MUPlan.enable_exchange) when every
+    shard is a persistent shape — fp32, F = 81, MU k = 4 or 8 (shard rows a multiple of 16 / 8),
+    the constrained ALS and the weighted MU at k = 4 (rows a multiple of 16) — and the buffers can
+    be shared; otherwise the RCCL path (one shard step + one all_reduce per iteration).
+    exchange=True: the same, with a warning when it falls back; exchange=False: always RCCL.
+    A launch that fails on any rank sends every rank back to the RCCL path (solver.sync_failed).
 
     weights: this rank's rows of the per-element weights (float32 X): the
     weighted / masked MU, whose 2kF accumulators [W'ᵀ(M∘X) | W'ᵀ(M∘(W'H))] are all-reduced the
@@ -61,6 +64,8 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     all-reduced before every H-step.  Both take exchange=True (fp32, F = 81, k = 4, rows a multiple
     of 16): one persistent launch per rank with the all-reduce inside it.
     """
+    if exchange not in ("auto", True, False):
+        raise ValueError(f"exchange must be 'auto', True or False, got {exchange!r}")
     if not (dist.is_available() and dist.is_initialized()):
         raise RuntimeError("factorise_sharded needs an initialised torch.distributed process group")
     group = group if group is not None else dist.group.WORLD
@@ -84,11 +89,17 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
         plan = MUPlan(X, H0.shape[0], l1_reg_W, l2_reg_W, l1_reg_H, l2_reg_H, group=group)
     plan.set_W(torch.as_tensor(W_shard))
     plan.set_H(H0)
-    if exchange:
+    if exchange == "auto" and update_H:
+        # every rank must take the same decision before the collective enable_exchange
+        from .solver import agree_max
+        if agree_max([0.0 if plan.persistent_shape else 1.0], group, plan.device)[0] != 0.0:
+            exchange = False
+    if exchange and update_H:
         try:
             plan.enable_exchange()
         except _lib.HipLibraryError as e:
-            warnings.warn(f"in-launch exchange not used: {e}", RuntimeWarning)
+            if exchange is True:
+                warnings.warn(f"in-launch exchange not used: {e}", RuntimeWarning)
     n_iter = run_mu(plan, max_iter=max_iter, tol=tol, update_H=update_H)
     plan.release()
     return plan.W, plan.H(), n_iter

@@ -23,6 +23,7 @@ import torch
 
 from . import _lib
 from ._lib import check
+from ._trace import trace_range
 
 _XDT = {torch.float32: _lib.F32, torch.float64: _lib.F64, torch.bfloat16: _lib.BF16}
 
@@ -122,8 +123,11 @@ class MUPlan:
         self.H64 = torch.zeros((self.k, self.F), dtype=f64, device=dev)
         self.Ht = torch.zeros((self.F, KP), dtype=f64, device=dev)
         self.HHt = torch.zeros((KP, KP), dtype=f64, device=dev)
-        self.partials = torch.zeros((max(self.n_parts, 1), self.n_out), dtype=f64, device=dev)
-        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out)), dtype=f64, device=dev)
+        # partial rows, stage and AB leave room for the loss column of the device tolerance test
+        # (cnmf_mu_fit_tol: rows of n_out + 1); the other launches use rows of n_out in the same memory
+        self._partials = torch.zeros(max(self.n_parts, 1) * (self.n_out + 1), dtype=f64, device=dev)
+        self.partials = self._partials[:max(self.n_parts, 1) * self.n_out].view(max(self.n_parts, 1), self.n_out)
+        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out + 1)), dtype=f64, device=dev)
         self.counter = torch.zeros(int(self.lib.cnmf_counter_words()), dtype=torch.int32, device=dev)
         self.err_word = int(self.lib.cnmf_counter_err_word())
         with torch.cuda.device(self.device):
@@ -133,9 +137,11 @@ class MUPlan:
         self.layout = 0  # layout of the persistent launch (include/cnmf_hip.h; 0 = default); tune() sets it
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
         self.exchange = False  # True: multi-GPU iterations as one launch per rank (enable_exchange)
-        self.AB = torch.zeros(self.n_out, dtype=f64, device=dev)
+        self._AB = torch.zeros(self.n_out + 1, dtype=f64, device=dev)
+        self.AB = self._AB[:self.n_out]
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)
+        self._wsnap = None  # the device tolerance test's W snapshot (streamed W), allocated on first use
 
     # -- multi-GPU with the all-reduce inside the launch ------------------------------------------
     def enable_exchange(self):
@@ -470,6 +476,44 @@ class MUPlan:
         self.check_sync_error()
         return ev[0].elapsed_time(ev[1]) / 1e3
 
+    # -- the tolerance test on the device (cnmf_mu_fit_tol) -----------------------------------------
+    _TC = {"tol": 0, "it0": 1, "init": 2, "prev": 3, "done": 4, "stopped": 5, "in_snap": 6, "wsnap": 7,
+           "cap": 8, "nerr": 9, "errs": 16}
+
+    def fit_device_tol(self, max_iter: int, tol: float, pass_events=None):
+        """max_iter MU iterations with sklearn's tolerance test (SK:872-884) evaluated on the device:
+        ONE launch, no host round trip per 10 iterations (cnmf_mu_fit_tol).  Returns
+        (n_iter, [(g, error)] for g = 0, 10, ... checked), or None when the library does not serve
+        this plan's shape (the caller then runs the host loop).  Synchronises once, at the end."""
+        import numpy as np
+        if not self.persistent or self.n_rows == 0 or tol <= 0:
+            return None
+        n_tc = int(check(self.lib.cnmf_tolctl_doubles(max_iter), "cnmf_tolctl_doubles"))
+        if self._wsnap is None or self._wsnap.shape != self.W.shape:
+            self._wsnap = torch.empty_like(self.W)
+        host = np.zeros(n_tc, dtype=np.float64)
+        host[self._TC["tol"]] = tol
+        host[self._TC["cap"]] = n_tc - self._TC["errs"]
+        host[self._TC["wsnap"]] = np.array([self._wsnap.data_ptr()], dtype=np.uint64).view(np.float64)[0]
+        tolctl = torch.from_numpy(host).to(self.device)
+        ev = _event_array(pass_events)
+        with torch.cuda.device(self.device):
+            st = self.lib.cnmf_mu_fit_tol(
+                max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self._AB),
+                _ptr(tolctl), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H,
+                self.layout, _ptr(self.xctl) if getattr(self, "exchange", False) else None, *ev, self._stream())
+        if st == -3:  # CNMF_ERR_UNSUPPORTED: not a wave-tile shape / layout
+            return None
+        check(st, "cnmf_mu_fit_tol")
+        out = tolctl.cpu().numpy()
+        n_done = int(out[self._TC["done"]])
+        if out[self._TC["stopped"]] != 0 and out[self._TC["in_snap"]] != 0:
+            self.W.copy_(self._wsnap)
+        nerr = int(out[self._TC["nerr"]])
+        errs = [(10 * i, float(out[self._TC["errs"] + i])) for i in range(min(nerr, n_tc - self._TC["errs"]))]
+        return n_done, errs
+
     _NORMS = {"l1": 1, "l2": 2, "max": 3}
 
     def normalise(self, norm: str = "l2") -> torch.Tensor:
@@ -538,27 +582,62 @@ def _iterate_guarded(plan, n_iter: int, update_H: bool):
         plan.check_sync_error()
 
 
+def _run_mu_device_tol(plan, max_iter, tol, verbose, return_errors):
+    """run_mu's tol > 0 fit as ONE launch with the test on the device; None when not served.  On a
+    failed launch (any rank) every rank restores its state and returns None (the host loop runs)."""
+    W0, H0 = plan.W.clone(), plan.H64.clone()
+    with trace_range(f"cnmf:iterations 1..{max_iter} (device tol)"):
+        res = plan.fit_device_tol(max_iter, tol)
+    if res is None:  # not served: nothing was launched
+        return None
+    if sync_failed(plan):
+        plan.W.copy_(W0)
+        plan.H64.copy_(H0)
+        plan.refresh_basis()
+        if getattr(plan, "exchange", False):
+            plan.disable_exchange()
+        plan.exchange = False
+        plan.persistent = False
+        return None
+    n_iter, errors = res
+    if (verbose or return_errors) and n_iter == max_iter and max_iter % 10 == 0:
+        errors.append((max_iter, plan.frobenius_error()))  # sklearn's check after the last iteration
+    if verbose:
+        for it, e in errors[1:]:
+            print(f"Epoch {it:02d} reached, error: {e:f}")
+    return n_iter, errors
+
+
 def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool = True,
            verbose: int = 0, return_errors: bool = False):
     """The driver of `_fit_multiplicative_update` (SK:731-893).  Returns n_iter (and the error
-    trajectory [(n_iter, error)] when return_errors)."""
+    trajectory [(n_iter, error)] when return_errors).  tol > 0 on a wave-tile persistent plan: ONE
+    launch with the tolerance test on the device (MUPlan.fit_device_tol); else stretches of 10
+    iterations with the error checked on the host between them."""
+    if tol > 0 and update_H and hasattr(plan, "fit_device_tol") and getattr(plan, "persistent", False):
+        res = _run_mu_device_tol(plan, max_iter, tol, verbose, return_errors)
+        if res is not None:
+            return res if return_errors else res[0]
     errors = []
     if tol > 0:
-        error_at_init = plan.frobenius_error()  # SK:827
+        with trace_range("cnmf:loss it=0"):
+            error_at_init = plan.frobenius_error()  # SK:827
         previous_error = error_at_init
         errors.append((0, error_at_init))
     it = 0
     while it < max_iter:
         stop = min(max_iter, (it // 10 + 1) * 10) if tol > 0 else max_iter
-        if getattr(plan, "persistent", False) and update_H:
-            _iterate_guarded(plan, stop - it, update_H)
-        else:
-            plan.iterate(stop - it, update_H)
-            if tol > 0 or stop >= max_iter:
-                plan.check_sync_error()
+        with trace_range(f"cnmf:iterations {it + 1}..{stop}"):
+            if getattr(plan, "persistent", False) and update_H:
+                _iterate_guarded(plan, stop - it, update_H)
+            else:
+                plan.iterate(stop - it, update_H)
+                if tol > 0 or stop >= max_iter:
+                    plan.check_sync_error()
         it = stop
         if tol > 0 and it % 10 == 0:  # SK:872-884
-            error = plan.frobenius_error()
+            with trace_range(f"cnmf:loss it={it}"):
+                error = plan.frobenius_error()
             errors.append((it, error))
             if verbose:
                 print(f"Epoch {it:02d} reached, error: {error:f}")
@@ -626,6 +705,9 @@ class ALSPlan(MUPlan):
 
     def tune(self, *args, **kwargs) -> dict:
         return {}  # one layout
+
+    def fit_device_tol(self, *args, **kwargs):
+        return None  # the tolerance test of the ALS runs on the host (its loss is not the MU pass's)
 
     def prepare(self, n_iter: int, pass_events=None):
         """As MUPlan.prepare, for the persistent ALS launch."""

@@ -188,6 +188,33 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
                              double l2_H, uint64_t* xctl, int layout, void* const* events, int n_events,
                              void* stream);
 
+/* ---- The tolerance test on the device (SK:872-884 without a host round trip).
+ * cnmf_mu_fit_tol runs up to max_iter MU iterations of the wave-tile launch (fp32 X, F = 81, k = 4
+ * or 8, layout 0 / 4; xctl NULL = one GPU, else the in-launch exchange as cnmf_mu_iterations_multi)
+ * as ONE launch that also evaluates ‖X − W·H‖ of the state after g iterations (g = it0, it0 + 10,
+ * ...: in the pass of iteration g + 1, which already reads x and w) and stops on the device when
+ * (previous − error) / error_at_init < tol — sklearn's n_iter, W and H exactly as its loop leaves
+ * them.  Buffers as cnmf_mu_iterations' except: partials rows, stage and AB hold k·(F+k) + 1
+ * doubles (the loss column); tolctl = cnmf_tolctl_doubles(max_iter) doubles with, set by the
+ * caller: [CNMF_TC_TOL] tol (> 0), [CNMF_TC_IT0] it0 (global index of the launch's first
+ * iteration; its errors go to slots g / 10), [CNMF_TC_CAP] error slots after CNMF_TC_ERRS,
+ * [CNMF_TC_WSNAP] a device buffer of n_rows·k floats (bits of the pointer; used when W is streamed,
+ * k = 8 past the LDS limit), and when it0 > 0 [CNMF_TC_INIT] / [CNMF_TC_PREV] from the previous
+ * launch.  Out: [CNMF_TC_DONE] iterations done (global), [CNMF_TC_STOPPED] 1 if the test stopped
+ * the fit, [CNMF_TC_IN_SNAP] 1 if the stopped fit's W is in the snapshot buffer (copy it to W),
+ * [CNMF_TC_NERR] and the checked errors from [CNMF_TC_ERRS].  The counter's flag word is cleared
+ * in stream order after the launch. */
+enum cnmf_tolctl_slots {
+  CNMF_TC_TOL = 0, CNMF_TC_IT0 = 1, CNMF_TC_INIT = 2, CNMF_TC_PREV = 3, CNMF_TC_DONE = 4, CNMF_TC_STOPPED = 5,
+  CNMF_TC_IN_SNAP = 6, CNMF_TC_WSNAP = 7, CNMF_TC_CAP = 8, CNMF_TC_NERR = 9, CNMF_TC_ERRS = 16
+};
+int cnmf_tolctl_doubles(int max_iter);
+int cnmf_mu_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                    double* partials, int64_t n_parts, double* stage, uint32_t* counter, double* AB,
+                    double* tolctl, int64_t n_rows, int n_features, int k, double l1_W, double l2_W,
+                    double l1_H, double l2_H, int layout, uint64_t* xctl, void* const* events, int n_events,
+                    void* stream);
+
 /* Normalisation projection (no sklearn counterpart, off unless asked for):
  *   s_j = ‖H_j‖ (norm 1 = L1, 2 = L2, 3 = max; s_j := 1 for an all-zero row),
  *   H_j <- H_j / s_j (H64, and Ht / HHt refreshed), W[:, j] <- W[:, j]·s_j, scale[j] = s_j,

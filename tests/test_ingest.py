@@ -43,4 +43,55 @@ def test_refusals(tmp_path):
     with pytest.raises(ValueError, match="no column"):
         load_spectra(q, device="cpu", columns=["f0", "nope"])
     with pytest.raises(ValueError, match="unsupported"):
-        load_spectra(tmp_path / "x.nc", device="cpu")
+        load_spectra(tmp_path / "x.h5", device="cpu")
+
+
+def _write_nc(path, cube, dims=("wavelength", "y", "x"), scale=None, offset=None, fill=None, dtype="f4"):
+    from scipy.io import netcdf_file
+    with netcdf_file(str(path), "w", version=2) as nc:
+        for d, n in zip(dims, cube.shape):
+            nc.createDimension(d, n)
+        if "wavelength" in dims:
+            nc.createVariable("wavelength", "f4", ("wavelength",))[:] = np.arange(cube.shape[0]) * 5 + 350.0
+        v = nc.createVariable("a", dtype, dims)
+        if scale is not None:
+            v.scale_factor = scale
+        if offset is not None:
+            v.add_offset = offset
+        if fill is not None:
+            v._FillValue = fill
+        v[:] = cube
+
+
+def test_netcdf3_cube_round_trip(tmp_path):
+    """An IOP cube a(wavelength, y, x) in a netCDF-3 file: samples = pixels in C order, columns =
+    wavelengths; chunking over the leading sample dimension reads back exactly."""
+    X = iop_spectra(6 * 7, 81, seed=4, dtype=np.float32)            # 42 pixels x 81 bands
+    cube = X.reshape(6, 7, 81).transpose(2, 0, 1).copy()           # (wavelength, y, x)
+    p = tmp_path / "iop.nc"
+    _write_nc(p, cube)
+    for chunk in (1, 7, 15, 1000):
+        t = load_spectra(p, device="cpu", chunk_rows=chunk)
+        np.testing.assert_array_equal(t.numpy(), X)
+    # the feature dimension named explicitly, a (y, x, band) layout
+    q = tmp_path / "iop2.nc"
+    _write_nc(q, X.reshape(6, 7, 81), dims=("y", "x", "band"))
+    np.testing.assert_array_equal(load_spectra(q, device="cpu", feature_dim="band").numpy(), X)
+
+
+def test_netcdf3_scale_offset_and_fill(tmp_path):
+    X = iop_spectra(20, 81, seed=5, dtype=np.float64)
+    cube = X.reshape(4, 5, 81).transpose(2, 0, 1)
+    packed = np.round((cube - 0.001) / 1e-4).astype(np.int16)     # packed shorts, as ocean products ship
+    packed[:, 1, 2] = -32767                                       # one land pixel
+    p = tmp_path / "packed.nc"
+    _write_nc(p, packed, scale=1e-4, offset=0.001, fill=-32767, dtype="h")
+    with pytest.raises(ValueError, match="NaN"):
+        load_spectra(p, device="cpu", dtype=np.float64)
+    t, rows = load_spectra(p, device="cpu", dtype=np.float64, drop_invalid=True)
+    assert t.shape == (19, 81) and 1 * 5 + 2 not in rows.tolist() and len(rows) == 19
+    sc, off = float(np.float32(1e-4)), float(np.float32(0.001))  # the file stores the attributes as floats
+    ref = (packed.transpose(1, 2, 0).reshape(20, 81).astype(np.float64) * sc + off)[rows]
+    np.testing.assert_allclose(t.numpy(), ref, rtol=0, atol=1e-15)
+    assert np.abs(np.delete(packed.reshape(81, -1), 7, axis=1)).max() < 32000
+    np.testing.assert_allclose(t.numpy(), X[rows], atol=6e-5)

@@ -77,6 +77,10 @@ def parse():
                         "tens of ms of work; the state is restored, the timed K steps are unchanged)")
     p.add_argument("--no-tune", action="store_true",
                    help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
+    p.add_argument("--tol", type=float, default=0.0,
+                   help="> 0: the timed fit runs sklearn's tolerance test (SK:872-884) on the device "
+                        "(cnmf_mu_fit_tol: ONE launch, the error every 10 iterations inside it); value = "
+                        "iterations done / time (the fit may stop before --steps)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend at N > 1: nccl (= RCCL over xGMI, the default) or "
                         "gloo (host-side collectives: lets two ranks share one GPU, as the N > 1 tests do)")
@@ -392,6 +396,8 @@ def main():
 
     K = args.steps
 
+    tol_result = {}
+
     def timed():
         persistent = plan.persistent and (world == 1 or plan.exchange)
         events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if persistent else 2 * K)]
@@ -399,7 +405,18 @@ def main():
         for e in events:  # creates the HIP events (outside the timed region)
             e.record(stream)
         # the K iterations' library call with its arguments marshalled here, outside the timed region
-        run = plan.prepare(K, pass_events=events)
+        prep = plan.prepare_device_tol(K, args.tol, pass_events=events) if (
+            args.tol > 0 and persistent and hasattr(plan, "prepare_device_tol")) else None
+        if args.tol > 0 and prep is None:
+            raise SystemExit("--tol needs a plan whose shape takes the device tolerance test (wave tiles)")
+        if prep is not None:
+            launch, finish = prep
+
+            def run():
+                launch()
+                tol_result["n_iter"], tol_result["errors"] = finish()  # the one synchronisation
+        else:
+            run = plan.prepare(K, pass_events=events)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -445,7 +462,7 @@ def main():
     sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
     sw = 8 if args.dtype == "f64" else 4
     bytes_per_pass = n_rows * (F * sx + 2 * k * sw) + (n_rows * F * 4 if args.weighted else 0)  # + M
-    iters_per_launch = K if persistent else 1
+    iters_per_launch = tol_result.get("n_iter", K) if persistent else 1
     bytes_per_launch = bytes_per_pass * iters_per_launch
     achieved = bytes_per_launch / avg_pass_s_max / 1e9
 
@@ -472,7 +489,8 @@ def main():
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
     elif persistent:
-        kbase = "mu_iter_wt_kernel" if "mu_iter_wt_kernel" in (layout or "") else "mu_iter_sl_kernel"
+        kbase = next((kn for kn in ("mu_iter_mf8_kernel", "mu_iter_wt_kernel") if kn in (layout or "")),
+                     "mu_iter_sl_kernel")
         if world == 1:
             kname = (f"{kbase} (persistent: K iterations of pass + in-launch reduction + basis "
                      "update per launch)")
@@ -502,10 +520,11 @@ def main():
         else:
             cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
 
+    K_done = tol_result.get("n_iter", K)  # --tol: the iterations the fit actually ran
     if args.scaling == "strong":
-        value = K / elapsed  # iterations per second of the whole (fixed) problem
+        value = K_done / elapsed  # iterations per second of the whole (fixed) problem
     else:
-        value = world * n_rows / 1e6 * K / elapsed
+        value = world * n_rows / 1e6 * K_done / elapsed
     if args.weighted:
         metric = "weighted MU iterations/sec (V=1e6x81 k=4 with per-element weights, 30 % zero)"
         workload = (f"weighted / masked MU (SURVEY 8f row 2, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
@@ -523,12 +542,12 @@ def main():
         if args.scaling == "strong":
             metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6\u00d781 k=4, 1/2/4/8 GPU"
                       if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
-            workload = (f"{cfg}: MU (Frobenius, tol=0) on V={args.rows}x{F} in total, k={k}, "
+            workload = (f"{cfg}: MU (Frobenius, tol={args.tol:g}) on V={args.rows}x{F} in total, k={k}, "
                         f"{args.dtype} synthetic IOP spectra, rows split over {world} GPU(s) in "
                         f"64-row-aligned shards (strong scaling: the problem is fixed)")
         else:
             metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
-            workload = (f"{cfg}: MU (Frobenius, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
+            workload = (f"{cfg}: MU (Frobenius, tol={args.tol:g}) on V={n_rows}x{F} per GPU, k={k}, "
                         f"{args.dtype} synthetic IOP spectra (weak scaling: every GPU owns this "
                         f"many rows)")
     out = {
@@ -538,7 +557,7 @@ def main():
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / K * 1e3, 4),
+        "ms_per_step": round(elapsed / max(tol_result.get("n_iter", K), 1) * 1e3, 4),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -555,7 +574,10 @@ def main():
                    "layout_per_rank": layouts,
                    "backend": (args.backend if dist_path else None),
                    "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None,
-                   "clock_ramp_s": round(ramp_s, 3), "clock_ramp_trips": ramp_trips},
+                   "clock_ramp_s": round(ramp_s, 3), "clock_ramp_trips": ramp_trips,
+                   "tol": args.tol or None,
+                   "tol_n_iter": tol_result.get("n_iter"),
+                   "tol_errors": tol_result.get("errors")},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "final_frobenius_error": err,

@@ -31,14 +31,18 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > out_m for d in deps if os.path.exists(d))
 
 
-def build(verbose: bool = False, force: bool = False, stamps: bool = False) -> str:
-    """Compile libcnmf_hip.so (or, with stamps=True, the diagnostic libcnmf_hip_stamps.so whose pass
-    kernel records per-phase s_memtime sums; never used by the product)."""
-    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
-    if not force and not stamps and not needs_build():
+def build(verbose: bool = False, force: bool = False, stamps: bool = False, diag: bool = False) -> str:
+    """Compile libcnmf_hip.so.  Diagnostic builds, never loaded by the product (select one with
+    CNMF_HIP_LIB=<path> in tools/ runs): stamps=True -> libcnmf_hip_stamps.so (in-kernel s_memtime /
+    s_memrealtime stamps: per-phase sums, persistent-launch timelines; implies diag); diag=True ->
+    libcnmf_hip_diag.so (the A/B environment switches CNMF_* and cnmf_hbm_probe)."""
+    out = OUT.replace(".so", "_stamps.so") if stamps else (OUT.replace(".so", "_diag.so") if diag else OUT)
+    if not force and not stamps and not diag and not needs_build():
         return OUT
     cmd = [hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared",
            "-I", os.path.join(ROOT, "include"), "-o", out + ".tmp", SRC]
+    if stamps or diag:
+        cmd.insert(1, "-DCNMF_DIAG")
     if stamps:
         cmd.insert(1, "-DCNMF_STAMPS")
     if verbose:
@@ -50,4 +54,4 @@ def build(verbose: bool = False, force: bool = False, stamps: bool = False) -> s
 
 if __name__ == "__main__":
     print(build(verbose="--verbose" in sys.argv, force="--force" in sys.argv,
-                stamps="--stamps" in sys.argv))
+                stamps="--stamps" in sys.argv, diag="--diag" in sys.argv))

@@ -2854,9 +2854,8 @@ __device__ __forceinline__ void xchg_allreduce_n(uint64_t* xctl, double* AB, dou
 
 // Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) and HHᵀ (fp64; lanes over f, fixed shuffle
 // tree) from the fp64 H in LDS — sl_derive_basis for k = KK
-template <int KK>
+template <int KK, class G = wt::Geo<KK>>
 __device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
-  using G = wt::Geo<KK>;
   const double* sH = reinterpret_cast<const double*>(smem + G::L_H);
   float* sHt = reinterpret_cast<float*>(smem + G::L_HT);
   double* sHHt = reinterpret_cast<double*>(smem + G::L_HHT);
@@ -2881,9 +2880,8 @@ __device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
 }
 // H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728) —
 // sl_update_basis for k = KK
-template <int KK>
+template <int KK, class G = wt::Geo<KK>>
 __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, double l1, double l2) {
-  using G = wt::Geo<KK>;
   constexpr int KF = KK * wt::F;
   constexpr int U = (KF + NT - 1) / NT;
   double* sH = reinterpret_cast<double*>(smem + G::L_H);
@@ -2911,7 +2909,7 @@ __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, doub
   for (int u = 0; u < U; ++u)
     if (t + NT * u < KF) sH[t + NT * u] = hn[u];
   __syncthreads();
-  wt_derive_basis<KK>(smem, t);
+  wt_derive_basis<KK, G>(smem, t);
 }
 
 // TOL: the tolerance test of SK:872-884 on the device.  In iteration g + 1 (g = it0 + it, g % 10 ==
@@ -3395,6 +3393,482 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       __syncthreads();
     }
     wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+    load_basis();
+    TL(it, 1);
+  };
+
+  for (int p = 0; p < total && alive; p += PD) {
+#pragma unroll
+    for (int k = 0; k < PD; ++k) {
+      step(pf[k]);
+      if (p + k < total && alive) body();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+}
+
+// ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// mu_iter_mf8_kernel<WRES, PD, MULTI, TOL> — k = 8 (cfg3) wave tiles on the matrix cores.
+//
+// The VALU wave-tile kernel at k = 8 is issue-bound (248 VALU per 8-sample tile against an FMA
+// minimum of 85: the fp32 products plus the DPP reduce-scatter, fp64 folds and division; DESIGN
+// §3.0).  Here both products run on v_mfma_f32_16x16x4_f32 (exact fp32 FMA chains at the f32
+// rate), which issue beside the VALU work left (folds, the fp64 update, addressing), so the pass
+// can become HBM-bound.  One wave owns 16-sample tiles (5184 B of X: the k = 4 tile geometry).
+//   phase 1  NUM[s][e] = Σ_f x[s][f]·H[e][f]     M = 16 samples, N = 16 (8 components), K = 84:
+//            21 K-steps in 7 independent chains of 3 (12 features each, ≤ the 14-rounding depth of
+//            the VALU path), each chain folded into fp64 (DESIGN §4's long-fp32-dot hazard).
+//            A = X[s = l&15][f = 4ks + l>>4] (LDS), B = Hᵀ[f][e = l&15] (21 VGPRs per basis).
+//   phase 2  DEN[s][e] = Σ_m w[s][m]·HHᵀ[m][e]    2 MFMAs (fp32, 8 terms as the VALU path); the
+//            update w·num/den in fp64 by the lanes e < 8 (4 samples each, the C layout
+//            col = e = l&15, row = s = 4(l>>4) + r), SK:553-629.
+//   phase 3  Aᵀ[f][n] = Σ_s [X | W'][s][f]·W'[s][n]   M = 16 features × 6 blocks (96 ≥ F + 8: the
+//            last block's rows 81..88 carry W', so it also yields WᵀW), N = 16 (8 components),
+//            K = 16 samples: 24 MFMAs in 6 independent accumulators, folded into fp64 every 16
+//            tiles (≤ 256 samples per fp32 chain).
+// W' reaches phase 3 through a [16][16] per-wave LDS image (columns ≥ 8 zero).  The prefetch /
+// staging (AGPR sets, counted waits), the W residency, the end-of-iteration reduction, the
+// in-launch exchange (MULTI) and the device tolerance test (TOL: ‖x − w·H‖² via 12 more MFMAs
+// R = W·H in the loss iterations) are mu_iter_wt_kernel's.
+// ------------------------------------------------------------------------------------------------
+namespace wt {
+typedef float f4v __attribute__((ext_vector_type(4)));
+struct GeoMF8 {
+  static constexpr int K = 8, TSW = 16, V = F + 8, NOUT = 8 * V;
+  static constexpr int NL = 8, NQ = 11;  // the sHt image wt_derive_basis<8> writes (Geo<8>'s)
+  static constexpr int XBW = TSW * F * 4;                  // 5184 B of X per tile
+  static constexpr int NCHW = XBW / 16;                    // 324 chunks
+  static constexpr int PFW = (NCHW + 63) / 64;             // 6 loads per lane
+  static constexpr int LASTL = NCHW - 64 * (PFW - 1);      // 4
+  static constexpr int PADB = 16;                          // phase 1 reads 3 floats past the tile
+  static constexpr int XSTR = XBW + PADB;
+  static constexpr int WBW = TSW * 8 * 4;                  // 512 B of W per tile
+  static constexpr int KS1 = 21, NCH1 = 7, NB3 = 6;
+  static constexpr int L_STG = 0;                                       // [NWV][XSTR]
+  static constexpr int L_WSTG = L_STG + NWV * XSTR;                     // streamed W: [NWV][WBW]
+  static constexpr int L_WP = (L_WSTG + NWV * WBW + 15) / 16 * 16;      // W' operand [NWV][16][16] fp32
+  static constexpr int L_RED = L_WP + NWV * 16 * 16 * 4;                // [NWV][8][V] fp64
+  static constexpr int L_H = L_RED + NWV * 8 * V * 8;                   // H fp64 [8][F]
+  static constexpr int L_AB = L_H + 8 * F * 8;                          // AB fp64 (+ the loss)
+  static constexpr int L_HT = L_AB + (NOUT + 2) * 8;                    // (wt_derive_basis' Hᵀ image)
+  static constexpr int L_HHT = L_HT + NL * NQ * 8 * 4;                  // HHᵀ fp64 [8][8]
+  static constexpr int L_FLAG = L_HHT + 8 * 8 * 8;                      // 8 ints
+  static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] fp64
+  static constexpr int L_WRES = (L_LOSS + 8 * NWV + 15) / 16 * 16;      // [NWV][nbt_max][WBW]
+  static_assert(NCHW * 16 == XBW && L_HT % 16 == 0 && L_RED % 16 == 0, "layout");
+  static_assert(NOUT * 8 >= NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
+};
+__device__ __forceinline__ f4v mfma4(float a, float b, f4v c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+}  // namespace wt
+
+template <bool WRES, int PD, bool MULTI = false, bool TOL = false>
+__global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
+  using namespace wt;
+  using G_ = GeoMF8;
+  constexpr int KK = 8, TSW = G_::TSW, V = G_::V, NOUT = G_::NOUT;
+  constexpr int NOUTT = NOUT + (TOL ? 1 : 0);
+  constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, PFW = G_::PFW, LASTL = G_::LASTL;
+  constexpr int PFS = PFW + (WRES ? 0 : 1);
+  constexpr int KS1 = G_::KS1, NCH1 = G_::NCH1, NB3 = G_::NB3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int lc = l & 15, lr = l >> 4;  // MFMA lane coordinates: column / row-group
+  const int b = blockIdx.x;
+  const int G = gridDim.x;
+  const int NW = NWV * G;
+  const int gw = NWV * b + w;
+  const int NG = a.n_groups;
+  const int g = b % NG;
+  const int gs = (G - g + NG - 1) / NG;
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(a.X);
+  unsigned char* Wb = reinterpret_cast<unsigned char*>(a.W);
+  const int nbt = (int)((a.n_tiles - gw + NW - 1) / NW);
+  const int nbt_max = (int)((a.n_tiles + NW - 1) / NW);
+  unsigned char* stg = smem + G_::L_STG + w * XSTR;
+  unsigned char* wstg = smem + G_::L_WSTG + w * WBW;
+  float* wp = reinterpret_cast<float*>(smem + G_::L_WP) + w * 256;  // W' [16][16]
+  float* wres = reinterpret_cast<float*>(smem + G_::L_WRES + (size_t)w * nbt_max * WBW);
+  double* red = reinterpret_cast<double*>(smem + G_::L_RED);
+  double* sH = reinterpret_cast<double*>(smem + G_::L_H);
+  double* sAB = reinterpret_cast<double*>(smem + G_::L_AB);
+  int* sFlag = reinterpret_cast<int*>(smem + G_::L_FLAG);
+  double* sLoss = reinterpret_cast<double*>(smem + G_::L_LOSS);
+  const int it0 = TOL ? (int)ld_sc1(a.tolctl + TC_IT0) : 0;
+  float* wsnap = (TOL && !WRES)
+                     ? reinterpret_cast<float*>(__double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP)))
+                     : nullptr;
+  double lossacc = 0.0;
+  uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
+  uint32_t* cnt_top = a.cnt + CNT_TOP;
+  uint32_t* flag = a.cnt + CNT_FLAG;
+  uint32_t* err = a.cnt + CNT_ERR;
+
+  for (int i = t; i < KK * F; i += NT) sH[i] = a.H64[i];
+  if (a.apply_first)
+    for (int i = t; i < NOUT; i += NT) sAB[i] = a.AB[i];
+  if (l < G_::PADB / 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
+  for (int i = l; i < 256; i += 64) wp[i] = 0.f;  // columns >= 8 stay zero for the launch
+  if (WRES)
+    for (int c = l; c < nbt * (WBW / 16); c += 64) {
+      const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
+      *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
+          *reinterpret_cast<const u32x4*>(Wb + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
+    }
+  __syncthreads();
+  if (a.apply_first)
+    wt_update_basis<KK, G_>(smem, t, a.l1H, a.l2H);
+  else
+    wt_derive_basis<KK, G_>(smem, t);
+
+  // MFMA operands of the basis: Hᵀ[f = 4ks + lr][e = lc] (phase 1), HHᵀ[m = 4ks + lr][e = lc]
+  // (DEN), H[m = 4ks + lr][f = 16 blk + lc] (TOL: R = W·H); zero past k = 8 / F
+  float hB[KS1], hhB[2], hR[TOL ? NB3 : 1][2];
+  auto load_basis = [&]() {
+    const double* sHHt = reinterpret_cast<const double*>(smem + G_::L_HHT);
+#pragma unroll
+    for (int ks = 0; ks < KS1; ++ks) {
+      const int f = 4 * ks + lr;
+      hB[ks] = (lc < KK && f < F) ? (float)sH[(lc & 7) * F + (f < F ? f : 0)] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) hhB[ks] = lc < KK ? (float)sHHt[(4 * ks + lr) * KK + (lc & 7)] : 0.f;
+    if constexpr (TOL)
+#pragma unroll
+      for (int blk = 0; blk < NB3; ++blk)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int f = 16 * blk + lc;
+          hR[blk][ks] = f < F ? (float)sH[(4 * ks + lr) * F + (f < F ? f : 0)] : 0.f;
+        }
+  };
+  load_basis();
+
+  // phase-3 accumulators: fp32 MFMA C (≤ 16 tiles), fp64 folds; lane holds Aᵀ[16 blk + 4 lr + r][lc]
+  f4v acc3[NB3];
+  double acc64[NB3][4];
+  auto zero32 = [&]() {
+#pragma unroll
+    for (int blk = 0; blk < NB3; ++blk) acc3[blk] = f4v{0.f, 0.f, 0.f, 0.f};
+  };
+  auto fold = [&]() {
+#pragma unroll
+    for (int blk = 0; blk < NB3; ++blk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc64[blk][r] += (double)acc3[blk][r];
+    zero32();
+  };
+  zero32();
+#pragma unroll
+  for (int blk = 0; blk < NB3; ++blk)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc64[blk][r] = 0.0;
+
+  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile) {
+    const unsigned char* xs = Xb + (size_t)tile * XBW + 16 * l;
+#pragma unroll
+    for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
+    ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
+    if (!WRES) ld16(pf[PFW], l < WBW / 16 ? Wb + (size_t)tile * WBW + 16 * l : xs);
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS]) {
+    const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
+    stage_rec<0, PFW - 1>(addr, pf);
+    if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
+    if (!WRES && l < WBW / 16) st16<0>((unsigned)(uintptr_t)(wstg + 16 * l), pf[PFW]);
+  };
+
+  const int total = a.n_iter * nbt;
+  u32x4 pf[PD][PFS];
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
+#pragma unroll
+  for (int k = 0; k < PD; ++k) {
+    prefetch(pf[k], gw + (int64_t)NW * k);
+    if (!WRES) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+  }
+  TL_START;
+
+  bool alive = true;
+  int cur_i = 0, cur_it = 0, nx_i = PD;
+  auto step = [&](u32x4 (&pfk)[PFS]) {
+    wait_set<PFS * (PD - 1) + (WRES ? 0 : PD), PFS>(pfk);
+    stage(pfk);
+    prefetch(pfk, gw + (int64_t)NW * nx_i);
+    if (++nx_i == nbt) nx_i = 0;
+  };
+  auto body = [&]() {
+    const int it = cur_it, i = cur_i;
+    if (++cur_i == nbt) {
+      cur_i = 0;
+      ++cur_it;
+    }
+    const bool last_it = it + 1 == a.n_iter;
+    const bool loss_it = TOL && ((it0 + it) % 10 == 0);
+    const int64_t tile = gw + (int64_t)NW * i;
+    const float* sx = reinterpret_cast<const float*>(stg);
+    float* wt_ = WRES ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);  // [16][8]
+    // ---- phase 1: NUM = X·Hᵀ on the matrix cores, 7 chains of 3 K-steps folded into fp64
+    f4v c1[NCH1];
+#pragma unroll
+    for (int c = 0; c < NCH1; ++c) c1[c] = f4v{0.f, 0.f, 0.f, 0.f};
+    {
+      const float* xa = sx + lc * F + lr;  // A = X[s = lc][f = 4 ks + lr]
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int c = 0; c < NCH1; ++c) {
+          const int ks = 3 * c + j;
+          c1[c] = mfma4(xa[4 * ks], hB[ks], c1[c]);
+        }
+    }
+    // ---- DEN = W·HHᵀ (A = W[s = lc][m = 4 ks + lr])
+    const float wa0 = wt_[lc * KK + lr], wa1 = wt_[lc * KK + 4 + lr];
+    f4v dn = mfma4(wa0, hhB[0], f4v{0.f, 0.f, 0.f, 0.f});
+    dn = mfma4(wa1, hhB[1], dn);
+    if (loss_it) {
+      // ‖x − w·H‖² of the state before this update: R = W·H (C[s = 4 lr + r][f = 16 blk + lc])
+      float l2 = 0.f;
+#pragma unroll
+      for (int blk = 0; blk < NB3; ++blk) {
+        f4v rr = mfma4(wa0, hR[blk][0], f4v{0.f, 0.f, 0.f, 0.f});
+        rr = mfma4(wa1, hR[blk][1], rr);
+        const int f = 16 * blk + lc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = sx[(4 * lr + r) * F + (f < F ? f : 0)];
+          const float d = f < F ? x - rr[r] : 0.f;
+          l2 = fmaf(d, d, l2);
+        }
+      }
+      lossacc += (double)l2;
+      // the W of that state (16 B per lane of the first 32): into W itself (resident W) or the
+      // snapshot buffer (streamed W); extra stores only make the counted waits stricter
+      if (l < WBW / 16) {
+        const u32x4 wv16 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wt_) + 16 * l);
+        unsigned char* dst = WRES ? Wb : reinterpret_cast<unsigned char*>(wsnap);
+        *reinterpret_cast<u32x4*>(dst + (size_t)tile * WBW + 16 * l) = wv16;
+      }
+    }
+    // ---- phase 2: the update of (s = 4 lr + r, e = lc) for e < 8, fp64 (SK:553-629)
+    {
+      const int e = lc & 7;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int s = 4 * lr + r;
+        const double num = ((((double)c1[0][r] + (double)c1[1][r]) + ((double)c1[2][r] + (double)c1[3][r])) +
+                            (((double)c1[4][r] + (double)c1[5][r]) + (double)c1[6][r]));
+        const double wold = (double)wt_[s * KK + e];
+        double den = (double)dn[r];
+        if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
+        if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
+        if (den == 0.0) den = EPS32;                // SK:620
+        const float wn = (float)(wold * (num / den));  // SK:622-629
+        if (lc < KK) {
+          wt_[s * KK + e] = wn;
+          wp[s * 16 + e] = wn;
+        }
+      }
+    }
+    if (!WRES) {  // the tile's new W to HBM: ONE 16-byte store instruction per body (the counted
+                  // waits), lanes 32..63 repeating lanes 0..31's identical writes
+      const int lw = l & 31;
+      *reinterpret_cast<u32x4*>(Wb + (size_t)tile * WBW + 16 * lw) =
+          *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wt_) + 16 * lw);
+    }
+    // ---- phase 3: Aᵀ += [X | W']ᵀ·W' (B = W'[s = 4 ks + lr][n = lc]; A = [X | W'][s][f = 16 blk + lc])
+    {
+      float bw[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) bw[ks] = wp[(4 * ks + lr) * 16 + lc];
+      const float* xb = sx + lr * F + lc;  // X[s = 4 ks + lr][f = 16 blk + lc]
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int blk = 0; blk < NB3; ++blk) {
+          float av;
+          if (blk < NB3 - 1) {
+            av = xb[4 * ks * F + 16 * blk];
+          } else {  // features 80..95: x[s][80], then W'[s][0..7] (-> WᵀW), then zero
+            const float xv = xb[4 * ks * F + 16 * blk - lc];  // x[s][80] (clamped address)
+            const float wv = wp[(4 * ks + lr) * 16 + ((lc - 1) & 7)];
+            av = lc == 0 ? xv : (lc <= KK ? wv : 0.f);
+          }
+          acc3[blk] = mfma4(av, bw[ks], acc3[blk]);
+        }
+    }
+    if ((i & 15) == 15) fold();  // ≤ 256 samples per fp32 chain
+    if (i + 1 != nbt) return;
+
+    // ---- end of this wave's iteration: its sums -> LDS [w][n][f] (fp64)
+    fold();
+    if (lc < KK)
+#pragma unroll
+      for (int blk = 0; blk < NB3; ++blk)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 16 * blk + 4 * lr + r;
+          if (f < V) red[(w * KK + lc) * V + f] = acc64[blk][r];
+        }
+#pragma unroll
+    for (int blk = 0; blk < NB3; ++blk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc64[blk][r] = 0.0;
+    if (TOL) {
+      const double v = wave_sum(lossacc);
+      if (l == 0) sLoss[w] = v;
+      lossacc = 0.0;
+    }
+    __syncthreads();
+    {
+      double* prow = a.partials + (size_t)b * NOUTT;
+      if (TOL && t == 0)
+        __hip_atomic_store(prow + NOUT, (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      for (int o = t; o < NOUT; o += NT) {
+        constexpr int WS = KK * V;  // wave stride
+        const double val = (red[o] + red[o + WS]) + (red[o + 2 * WS] + red[o + 3 * WS]);
+        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
+    __syncthreads();
+    TL(it, 0);
+    if (t == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(cnt_group, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
+      sFlag[1] = 0;
+      sFlag[2] = 1;
+      sFlag[3] = 0;
+    }
+    __syncthreads();
+    // the last iteration of the launch waits for the flag too when it checks the tolerance (a stop
+    // there must reach every workgroup before it writes W back)
+    const bool must_wait = !last_it || loss_it;
+    if (sFlag[0]) {  // group combiner
+      sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
+      }
+      __syncthreads();
+      if (sFlag[1]) {  // top combiner: AB
+        sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
+        if (TOL && loss_it && t == 0) {  // SK:872-884 on the state after it0 + it iterations
+          const int gi = it0 + it;
+          const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+          const int slot = gi / 10;
+          if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
+          st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
+          if (gi == 0) {
+            st_sc1(a.tolctl + TC_INIT, errv);
+            st_sc1(a.tolctl + TC_PREV, errv);
+          } else {
+            const double init = ld_sc1(a.tolctl + TC_INIT), prev = ld_sc1(a.tolctl + TC_PREV);
+            if ((prev - errv) / init < ld_sc1(a.tolctl + TC_TOL))
+              sFlag[3] = 1;
+            else
+              st_sc1(a.tolctl + TC_PREV, errv);
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0 && must_wait)
+          __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        TL_PUB(it);
+      }
+    }
+    const bool top = sFlag[1] != 0;
+    if (!top && must_wait) {
+      if (t == 0) {
+        const uint32_t want = (uint32_t)(it + 1);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t f;
+        while (((f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~FLAG_STOP) < want) {
+          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+            sFlag[2] = 0;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sFlag[2] = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (TOL && (f & FLAG_STOP)) sFlag[3] = 1;
+      }
+      __syncthreads();
+      if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
+        alive = false;
+        return;
+      }
+    }
+    if (TOL && sFlag[3]) {
+      // stopped by the tolerance test: the state after it0 + it iterations (W already where it
+      // belongs, H = sH not updated); the host clears the flag word after the launch
+      alive = false;
+      if (!top) return;
+      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < F * KK; o += NT) {
+        const int f = o / KK;
+        const int j = o - f * KK;
+        a.Ht[o] = sH[j * F + f];
+      }
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
+        st_sc1(a.tolctl + TC_STOPPED, 1.0);
+        st_sc1(a.tolctl + TC_IN_SNAP, WRES ? 0.0 : 1.0);
+        if (MULTI)
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (last_it) {
+      alive = false;
+      if (WRES)  // this wave's W back to HBM, once per launch
+        for (int c = l; c < nbt * (WBW / 16); c += 64) {
+          const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+          *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+              *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
+        }
+      if (!top) return;
+      // the last combiner of the launch: every other workgroup has arrived for the last time
+      if (a.apply_last) wt_update_basis<KK, G_>(smem, t, a.l1H, a.l2H);
+      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < F * KK; o += NT) {
+        const int f = o / KK;
+        const int j = o - f * KK;
+        a.Ht[o] = sH[j * F + f];
+      }
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!must_wait)  // (else workgroups may still poll it: the host clears it after the launch)
+          __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (TOL) {
+          st_sc1(a.tolctl + TC_DONE, (double)(it0 + a.n_iter));
+          st_sc1(a.tolctl + TC_STOPPED, 0.0);
+        }
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      __syncthreads();
+    }
+    wt_update_basis<KK, G_>(smem, t, a.l1H, a.l2H);
     load_basis();
     TL(it, 1);
   };
@@ -6021,14 +6495,14 @@ static int default_layout() {
 }
 static int resolve_layout(int layout) {
   if (layout == 0) return default_layout();
-  return (layout >= 1 && layout <= 4) ? layout : -1;
+  return (layout >= 1 && layout <= 5) ? layout : -1;
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
-      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles) " \
-                     "or 4 (wave tiles)");                                                                  \
+      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles), " \
+                     "4 (wave tiles) or 5 (k = 8 wave tiles without matrix cores)");                       \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
@@ -6104,6 +6578,17 @@ static PassFn wt_fn_k(int pd, bool multi, bool tol) {
   return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false>);
 }
 }
+static PassFn mf8_fn(bool wres, bool multi, bool tol) {
+  if (wres)
+    return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, true, true>)
+                        : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, false, true>))
+               : (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, true, false>)
+                        : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, false, false>));
+  return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, true, true>)
+                      : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, true>))
+             : (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, true, false>)
+                      : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, false>));
+}
 static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false) {
   const int pd = tol ? 3 : wt_pd(k, wres, multi);
   if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol) : wt_fn_k<4, false>(pd, multi, tol);
@@ -6120,6 +6605,7 @@ struct WtLaunch {
   PassFn fn;
   int64_t G, n_tiles;
   size_t lds;
+  bool mf;  // k = 8 on the matrix cores (mu_iter_mf8_kernel)
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
@@ -6127,9 +6613,14 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
                     bool tol = false) {
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
   if (k == 4 && layout != 4) return false;
-  const int tsw = 64 / k, wbw = tsw * k * 4;
+  if (k == 8 && layout != 4 && layout != 5) return false;
+  // k = 8, layout 4: the matrix-core wave tiles (16-sample tiles); layout 5 (or rows not a multiple
+  // of 16): the VALU wave tiles (8-sample tiles)
+  const bool mf = k == 8 && layout == 4 && n_rows % 16 == 0;
+  const int tsw = mf ? 16 : 64 / k, wbw = tsw * k * 4;
   if (n_rows % tsw != 0) return false;
-  const size_t l_wres = k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES;
+  const size_t l_wres = mf ? (size_t)wt::GeoMF8::L_WRES
+                           : (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES);
   const int ncu = device_cus();
   const int64_t n_tiles = n_rows / tsw;
   for (int wres = 1; wres >= 0; --wres) {
@@ -6141,9 +6632,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
     if (lds > kMaxLds) continue;
-    const PassFn fn = wt_fn(k, wres != 0, multi, tol);
+    const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
-    *out = WtLaunch{fn, G, n_tiles, lds};
+    *out = WtLaunch{fn, G, n_tiles, lds, mf};
     return true;
   }
   return false;
@@ -6324,11 +6815,19 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
   RESOLVE_LAYOUT(layout);
   WtLaunch L;
   if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L)) {
-    const bool wres = L.lds > (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES);
-    snprintf(out, (size_t)len,
-             "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
-             "(%lld workgroups), no barrier inside an iteration",
-             k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
+    const bool wres = L.lds > (L.mf ? (size_t)wt::GeoMF8::L_WRES
+                                    : (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES));
+    if (L.mf)
+      snprintf(out, (size_t)len,
+               "mu_iter_mf8_kernel<k=8, W %s, PD=3>: matrix-core wave tiles of 16 samples "
+               "(v_mfma_f32_16x16x4_f32), one 4-wave workgroup per CU (%lld workgroups), no barrier inside "
+               "an iteration",
+               wres ? "resident in LDS" : "streamed with X", (long long)L.G);
+    else
+      snprintf(out, (size_t)len,
+               "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
+               "(%lld workgroups), no barrier inside an iteration",
+               k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
     return 1;
   }
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);

@@ -480,13 +480,14 @@ class MUPlan:
     _TC = {"tol": 0, "it0": 1, "init": 2, "prev": 3, "done": 4, "stopped": 5, "in_snap": 6, "wsnap": 7,
            "cap": 8, "nerr": 9, "errs": 16}
 
-    def fit_device_tol(self, max_iter: int, tol: float, pass_events=None):
-        """max_iter MU iterations with sklearn's tolerance test (SK:872-884) evaluated on the device:
-        ONE launch, no host round trip per 10 iterations (cnmf_mu_fit_tol).  Returns
-        (n_iter, [(g, error)] for g = 0, 10, ... checked), or None when the library does not serve
-        this plan's shape (the caller then runs the host loop).  Synchronises once, at the end."""
+    def prepare_device_tol(self, max_iter: int, tol: float, pass_events=None):
+        """(run, finish) for a max_iter fit with the tolerance test on the device (cnmf_mu_fit_tol):
+        run() issues the ONE launch (arguments marshalled and the control block on the device
+        beforehand), finish() synchronises and returns (n_iter, [(g, error)] for g = 0, 10, ...
+        checked), restoring W from the snapshot when the test stopped a streamed-W fit.  None when
+        the library does not serve this plan's shape (the caller runs the host loop)."""
         import numpy as np
-        if not self.persistent or self.n_rows == 0 or tol <= 0:
+        if not self.persistent or self.n_rows == 0 or tol <= 0 or max_iter <= 0:
             return None
         n_tc = int(check(self.lib.cnmf_tolctl_doubles(max_iter), "cnmf_tolctl_doubles"))
         if self._wsnap is None or self._wsnap.shape != self.W.shape:
@@ -496,23 +497,48 @@ class MUPlan:
         host[self._TC["cap"]] = n_tc - self._TC["errs"]
         host[self._TC["wsnap"]] = np.array([self._wsnap.data_ptr()], dtype=np.uint64).view(np.float64)[0]
         tolctl = torch.from_numpy(host).to(self.device)
-        ev = _event_array(pass_events)
-        with torch.cuda.device(self.device):
-            st = self.lib.cnmf_mu_fit_tol(
-                max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+        xctl = _ptr(self.xctl) if getattr(self, "exchange", False) else None
+        args = (max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
                 _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self._AB),
                 _ptr(tolctl), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H,
-                self.layout, _ptr(self.xctl) if getattr(self, "exchange", False) else None, *ev, self._stream())
-        if st == -3:  # CNMF_ERR_UNSUPPORTED: not a wave-tile shape / layout
+                self.layout, xctl, *_event_array(pass_events), self._stream())
+        fn = self.lib.cnmf_mu_fit_tol
+        cargs = tuple(None if a is None else t(a) if not isinstance(a, ctypes.Array) else a
+                      for a, t in zip(args, fn.argtypes))
+        with torch.cuda.device(self.device):
+            probe = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, self.layout,
+                                                     int(xctl is not None))
+        if probe <= 0 or "wave tiles" not in self.describe():
+            return None  # not a wave-tile shape / layout: the host loop
+        state = {}
+
+        def run():
+            if torch.cuda.current_device() != self.device.index:
+                with torch.cuda.device(self.device):
+                    state["st"] = fn(*cargs)
+            else:
+                state["st"] = fn(*cargs)
+
+        def finish():
+            check(state.get("st", -1), "cnmf_mu_fit_tol")
+            out = tolctl.cpu().numpy()
+            if out[self._TC["stopped"]] != 0 and out[self._TC["in_snap"]] != 0:
+                self.W.copy_(self._wsnap)
+            nerr = min(int(out[self._TC["nerr"]]), n_tc - self._TC["errs"])
+            return int(out[self._TC["done"]]), [(10 * i, float(out[self._TC["errs"] + i])) for i in range(nerr)]
+        return run, finish
+
+    def fit_device_tol(self, max_iter: int, tol: float, pass_events=None):
+        """max_iter MU iterations with sklearn's tolerance test (SK:872-884) evaluated on the device:
+        ONE launch, no host round trip per 10 iterations (cnmf_mu_fit_tol).  Returns
+        (n_iter, [(g, error)] for g = 0, 10, ... checked), or None when the library does not serve
+        this plan's shape (the caller then runs the host loop).  Synchronises once, at the end."""
+        prep = self.prepare_device_tol(max_iter, tol, pass_events)
+        if prep is None:
             return None
-        check(st, "cnmf_mu_fit_tol")
-        out = tolctl.cpu().numpy()
-        n_done = int(out[self._TC["done"]])
-        if out[self._TC["stopped"]] != 0 and out[self._TC["in_snap"]] != 0:
-            self.W.copy_(self._wsnap)
-        nerr = int(out[self._TC["nerr"]])
-        errs = [(10 * i, float(out[self._TC["errs"] + i])) for i in range(min(nerr, n_tc - self._TC["errs"]))]
-        return n_done, errs
+        run, finish = prep
+        run()
+        return finish()
 
     _NORMS = {"l1": 1, "l2": 2, "max": 3}
 

@@ -12,7 +12,7 @@ import sys
 
 def main(path):
     s = open(path).read()
-    names = re.findall(r"^(_ZN4cnmf17mu_iter_wt_kernel\w+|_Z18wmu_iter_wt_kernel\w+|_Z18als_iter_wt_kernel\w+):", s, re.M)
+    names = re.findall(r"^(_ZN4cnmf17mu_iter_wt_kernel\w+|_ZN4cnmf18mu_iter_mf8_kernel\w+|_Z18wmu_iter_wt_kernel\w+|_Z18als_iter_wt_kernel\w+):", s, re.M)
     bad_total = 0
     for name in names:
         i = s.index(name + ":")

@@ -2650,8 +2650,8 @@ struct Geo {
   static constexpr int L_HT = L_AB + (NOUT + 2) * 8;                    // Hᵀ fp32 [NL·NQ][K]
   static constexpr int L_HHT = L_HT + NL * NQ * KK * 4;                 // HHᵀ fp64 [K][K]
   static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 8 ints
-  static constexpr int L_LOSS = L_FLAG + 32;                            // the waves' loss sums [NWV] fp64
-  static constexpr int L_WRES = (L_LOSS + 8 * NWV + 15) / 16 * 16;      // [NWV][nbt_max][WBW]
+  static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] wave loss sums, init, prev
+  static constexpr int L_WRES = (L_LOSS + 8 * 8 + 15) / 16 * 16;        // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
   static_assert(OVR >= 0 && PADB / 4 <= 64, "one zero float per lane covers the overrun");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
@@ -2956,6 +2956,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   double* sLoss = reinterpret_cast<double*>(smem + G_::L_LOSS);
   // TOL: the launch's first global iteration, the snapshot buffer (streamed W)
   const int it0 = TOL ? (int)ld_sc1(a.tolctl + TC_IT0) : 0;
+  // TOL: every workgroup tracks the test's error at init and previous error itself (sLoss[4], [5]),
+  // so the decision of the iteration's top combiner reads no state another workgroup wrote
+  const double tolv = TOL ? ld_sc1(a.tolctl + TC_TOL) : 0.0;
+  if (TOL && t == 0) {
+    sLoss[4] = ld_sc1(a.tolctl + TC_INIT);
+    sLoss[5] = ld_sc1(a.tolctl + TC_PREV);
+  }
   float* wsnap = (TOL && !WRES)
                      ? reinterpret_cast<float*>(__double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP)))
                      : nullptr;
@@ -3289,14 +3296,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
           if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
           st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
           if (gi == 0) {
+            sLoss[4] = sLoss[5] = errv;
             st_sc1(a.tolctl + TC_INIT, errv);
             st_sc1(a.tolctl + TC_PREV, errv);
+          } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
+            sFlag[3] = 1;
           } else {
-            const double init = ld_sc1(a.tolctl + TC_INIT), prev = ld_sc1(a.tolctl + TC_PREV);
-            if ((prev - errv) / init < ld_sc1(a.tolctl + TC_TOL))
-              sFlag[3] = 1;
-            else
-              st_sc1(a.tolctl + TC_PREV, errv);
+            sLoss[5] = errv;
+            st_sc1(a.tolctl + TC_PREV, errv);
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3389,8 +3396,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       return;
     }
     if (!top) {
-      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
+      if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
+        const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+        if (it0 + it == 0) sLoss[4] = errv;
+        sLoss[5] = errv;
+      }
     }
     wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
     load_basis();
@@ -3454,8 +3466,8 @@ struct GeoMF8 {
   static constexpr int L_HT = L_AB + (NOUT + 2) * 8;                    // (wt_derive_basis' Hᵀ image)
   static constexpr int L_HHT = L_HT + NL * NQ * 8 * 4;                  // HHᵀ fp64 [8][8]
   static constexpr int L_FLAG = L_HHT + 8 * 8 * 8;                      // 8 ints
-  static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] fp64
-  static constexpr int L_WRES = (L_LOSS + 8 * NWV + 15) / 16 * 16;      // [NWV][nbt_max][WBW]
+  static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] wave loss sums, init, prev
+  static constexpr int L_WRES = (L_LOSS + 8 * 8 + 15) / 16 * 16;        // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && L_HT % 16 == 0 && L_RED % 16 == 0, "layout");
   static_assert(NOUT * 8 >= NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
 };
@@ -3497,6 +3509,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
   int* sFlag = reinterpret_cast<int*>(smem + G_::L_FLAG);
   double* sLoss = reinterpret_cast<double*>(smem + G_::L_LOSS);
   const int it0 = TOL ? (int)ld_sc1(a.tolctl + TC_IT0) : 0;
+  // TOL: every workgroup tracks the test's error at init and previous error itself (sLoss[4], [5]),
+  // so the decision of the iteration's top combiner reads no state another workgroup wrote
+  const double tolv = TOL ? ld_sc1(a.tolctl + TC_TOL) : 0.0;
+  if (TOL && t == 0) {
+    sLoss[4] = ld_sc1(a.tolctl + TC_INIT);
+    sLoss[5] = ld_sc1(a.tolctl + TC_PREV);
+  }
   float* wsnap = (TOL && !WRES)
                      ? reinterpret_cast<float*>(__double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP)))
                      : nullptr;
@@ -3765,14 +3784,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
           if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
           st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
           if (gi == 0) {
+            sLoss[4] = sLoss[5] = errv;
             st_sc1(a.tolctl + TC_INIT, errv);
             st_sc1(a.tolctl + TC_PREV, errv);
+          } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
+            sFlag[3] = 1;
           } else {
-            const double init = ld_sc1(a.tolctl + TC_INIT), prev = ld_sc1(a.tolctl + TC_PREV);
-            if ((prev - errv) / init < ld_sc1(a.tolctl + TC_TOL))
-              sFlag[3] = 1;
-            else
-              st_sc1(a.tolctl + TC_PREV, errv);
+            sLoss[5] = errv;
+            st_sc1(a.tolctl + TC_PREV, errv);
           }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3865,8 +3884,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
       return;
     }
     if (!top) {
-      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
+      if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
+        const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+        if (it0 + it == 0) sLoss[4] = errv;
+        sLoss[5] = errv;
+      }
     }
     wt_update_basis<KK, G_>(smem, t, a.l1H, a.l2H);
     load_basis();

@@ -43,11 +43,15 @@ def test_device_tol_matches_oracle(n, k, tol, max_iter):
     assert plan.counters_at_rest()
     Wr, Hr, nr, er = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
                                    max_iter=max_iter, tol=tol, return_errors=True)
+    ref = dict(er)
+    if n_iter != nr:  # diagnostics: the device's checked errors and decreases against the oracle's
+        for (g, e), (_, ep) in zip(errs[1:], errs):
+            print(f"g={g}: device {e:.9g} oracle {ref.get(g, float('nan')):.9g} "
+                  f"decrease {(ep - e) / errs[0][1]:.6g}")
     assert n_iter == nr, (n_iter, nr)
     W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
     # the checked errors: the oracle's (g, error) for every g the launch checked
-    ref = dict(er)
     for g, e in errs:
         assert abs(e - ref[g]) <= 1e-5 * ref[g], (g, e, ref[g])
     # Ht / HHt of the final H for the calls that follow

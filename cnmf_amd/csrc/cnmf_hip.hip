@@ -3289,6 +3289,9 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // (after the barrier: the summed loss sAB[NOUT] was written by another thread)
         if (TOL && loss_it && t == 0) {  // SK:872-884 on the state after it0 + it iterations
           const int gi = it0 + it;
           const double errv = sqrt(fmax(sAB[NOUT], 0.0));
@@ -3306,8 +3309,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
             st_sc1(a.tolctl + TC_PREV, errv);
           }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (TOL && loss_it) __syncthreads();  // sFlag[3] (the decision) for the whole workgroup
         if (t == 0 && must_wait)
           __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -3777,6 +3779,9 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // (after the barrier: the summed loss sAB[NOUT] was written by another thread)
         if (TOL && loss_it && t == 0) {  // SK:872-884 on the state after it0 + it iterations
           const int gi = it0 + it;
           const double errv = sqrt(fmax(sAB[NOUT], 0.0));
@@ -3794,8 +3799,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
             st_sc1(a.tolctl + TC_PREV, errv);
           }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        if (TOL && loss_it) __syncthreads();  // sFlag[3] (the decision) for the whole workgroup
         if (t == 0 && must_wait)
           __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);

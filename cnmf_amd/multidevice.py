@@ -15,8 +15,12 @@ the plans' collectives go through a `LocalGroup` instead of torch.distributed:
 
 The host thread per device only issues launches; the GIL is released while a thread waits on its
 device.  Results equal the one-device fit to fp64 summation order (tests/test_gpu_multidevice.py).
-Entries of `devices` may repeat (two logical shards on one GPU): the exchange is then used only if
-the shards' persistent grids fit on that GPU at the same time.
+Entries of `devices` may repeat (two logical shards on one GPU, e.g. for testing): those shards
+take the host all-reduce path by default, because HIP does not promise that two launches on
+different streams of ONE device run concurrently (streams share the device's few hardware queues),
+and the exchange needs every shard's launch resident at once; `shared_device_exchange=True` tries
+it anyway when the grids fit together (a launch that waits in vain times out and every shard
+falls back to the host all-reduce, with the same result).
 """
 from __future__ import annotations
 
@@ -97,11 +101,13 @@ def _device(d) -> torch.device:
     return torch.device("cuda", int(d))
 
 
-def _exchange_fits(plans) -> bool:
+def _exchange_fits(plans, shared_device_exchange=False) -> bool:
     """Every shard a persistent shape, and on each device the shards' persistent grids together
     within the CUs (one resident wave-tile workgroup per CU): co-running launches on one device all
     have to be resident, or the exchange would wait for a launch that cannot start."""
     if not all(getattr(p, "persistent_shape", False) for p in plans):
+        return False
+    if len({p.device.index for p in plans}) < len(plans) and not shared_device_exchange:
         return False
     if not all(type(p).__name__ == "MUPlan" for p in plans):
         return len({p.device.index for p in plans}) == len(plans)  # ALS / weighted: distinct devices
@@ -119,7 +125,7 @@ class MultiDeviceFit:
     """The shard plans of one fit over `devices` and the threads that drive them."""
 
     def __init__(self, X, Mw, k, regs, devices, *, solver="mu", sum_to_one=None, smoothness=0.0,
-                 align=64):
+                 align=64, shared_device_exchange=False):
         from .api import _make_plan
         self.devices = [_device(d) for d in devices]
         P = len(self.devices)
@@ -136,6 +142,7 @@ class MultiDeviceFit:
                                              group=self.group.view(r)))
         self.streams = [torch.cuda.Stream(p.device) for p in self.plans]
         self.exchange = False
+        self.shared_device_exchange = bool(shared_device_exchange)
 
     def _run(self, fn):
         """fn(rank, plan) on every shard's thread, with its device and stream current; re-raises the
@@ -170,7 +177,7 @@ class MultiDeviceFit:
         self._run(go)
 
     def enable_exchange(self):
-        if len(self.plans) == 1 or not _exchange_fits(self.plans):
+        if len(self.plans) == 1 or not _exchange_fits(self.plans, self.shared_device_exchange):
             return False
         try:
             self._run(lambda r, plan: plan.enable_exchange())

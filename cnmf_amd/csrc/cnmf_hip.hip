@@ -2929,6 +2929,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, NACC = G_::NACC;
   constexpr int PFW = G_::PFW, LASTL = G_::LASTL;
   constexpr int PFS = PFW + (WRES ? 0 : 1);  // loads per prefetch set (+ the W tile when streamed)
+  constexpr int NSTB = (WRES ? 0 : 1) + (TOL ? 1 : 0);  // stores per body (W streamed; TOL's snapshot)
   constexpr int KP = KK / 2;                 // component pairs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
@@ -3054,7 +3055,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
-    if (!WRES) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+#pragma unroll
+    for (int d = 0; d < NSTB; ++d) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
   }
   // W streamed: a tile's W store (body x) must have retired before its next load is issued (the
   // prefetch at step x + nbt - PD); the step waits retire every operation older than the set they
@@ -3068,9 +3070,10 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // first tile again, never used), so the count of younger loads is the same on every path.
   int cur_i = 0, cur_it = 0, nx_i = PD;
   auto step = [&](u32x4 (&pfk)[PFS]) {
-    // younger than this set's loads: the PD-1 later sets and, with W streamed, the W stores of the
-    // PD bodies since (one each; for the launch's first PD sets the prologue's dummy stores)
-    wait_set<PFS * (PD - 1) + (WRES ? 0 : PD), PFS>(pfk);
+    // younger than this set's loads: the PD-1 later sets and the stores of the PD bodies since
+    // (for the launch's first PD sets the prologue's dummy stores): with W streamed its W store, and
+    // TOL the snapshot store every body issues (a loss iteration's W, else a dummy)
+    wait_set<PFS * (PD - 1) + NSTB * PD, PFS>(pfk);
     stage(pfk);
     prefetch(pfk, gw + (int64_t)NW * nx_i);
     if (++nx_i == nbt) nx_i = 0;
@@ -3164,6 +3167,16 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     const float wold32 = wt_[s * KK + e];
     const double wold = (double)wold32;
+    if constexpr (TOL) {
+      // the W of the state a loss iteration checks, ONE store per body in every iteration (the
+      // steps' waits count it): a loss iteration stores the tile's W into W itself (resident W: HBM
+      // is not read again in this launch) or the snapshot buffer (streamed W); the others store the
+      // same value over the wave's first tile there, which the next loss iteration or the launch's
+      // write-back overwrites (a stop happens only at the end of a loss iteration)
+      const int64_t tsel = loss_it ? tile : (int64_t)gw;
+      float* snap = WRES ? reinterpret_cast<float*>(Wb) : wsnap;
+      snap[(size_t)tsel * TSW * KK + l] = wold32;
+    }
     if (loss_it) {
       // ‖x − w·H‖² of the state before this update, the lane's NQ features (the last lane's overrun
       // features past F belong to the next sample: masked)
@@ -3177,12 +3190,6 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
         l2 = fmaf(r, r, l2);
       }
       lossacc += (double)l2;
-      // the W of that state: into W itself (resident W: HBM is not read again in this launch) or
-      // the snapshot buffer (streamed W).  Extra stores only make the counted waits stricter.
-      if (WRES)
-        reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wold32;
-      else
-        wsnap[(size_t)tile * TSW * KK + l] = wold32;
     }
     double den = 0.0;
     if constexpr (KK == 8) {
@@ -3484,6 +3491,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
   constexpr int NOUTT = NOUT + (TOL ? 1 : 0);
   constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, PFW = G_::PFW, LASTL = G_::LASTL;
   constexpr int PFS = PFW + (WRES ? 0 : 1);
+  constexpr int NSTB = (WRES ? 0 : 1) + (TOL ? 1 : 0);  // stores per body (W streamed; TOL's snapshot)
   constexpr int KS1 = G_::KS1, NCH1 = G_::NCH1, NB3 = G_::NB3;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
@@ -3607,14 +3615,15 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);
-    if (!WRES) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+#pragma unroll
+    for (int d = 0; d < NSTB; ++d) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
   }
   TL_START;
 
   bool alive = true;
   int cur_i = 0, cur_it = 0, nx_i = PD;
   auto step = [&](u32x4 (&pfk)[PFS]) {
-    wait_set<PFS * (PD - 1) + (WRES ? 0 : PD), PFS>(pfk);
+    wait_set<PFS * (PD - 1) + NSTB * PD, PFS>(pfk);  // (the stores per body: mu_iter_wt_kernel's step)
     stage(pfk);
     prefetch(pfk, gw + (int64_t)NW * nx_i);
     if (++nx_i == nbt) nx_i = 0;
@@ -3664,12 +3673,17 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
         }
       }
       lossacc += (double)l2;
-      // the W of that state (16 B per lane of the first 32): into W itself (resident W) or the
-      // snapshot buffer (streamed W); extra stores only make the counted waits stricter
+    }
+    if constexpr (TOL) {
+      // the W of the checked state (16 B per lane of the first 32), ONE store per body in every
+      // iteration (counted by the steps' waits): a loss iteration's into W itself (resident W) or
+      // the snapshot buffer (streamed W), the others' over the wave's first tile there (overwritten
+      // by the next loss iteration or the launch's write-back; mu_iter_wt_kernel's snapshot)
       if (l < WBW / 16) {
         const u32x4 wv16 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wt_) + 16 * l);
         unsigned char* dst = WRES ? Wb : reinterpret_cast<unsigned char*>(wsnap);
-        *reinterpret_cast<u32x4*>(dst + (size_t)tile * WBW + 16 * l) = wv16;
+        const int64_t tsel = loss_it ? tile : (int64_t)gw;
+        *reinterpret_cast<u32x4*>(dst + (size_t)tsel * WBW + 16 * l) = wv16;
       }
     }
     // ---- phase 2: the update of (s = 4 lr + r, e = lc) for e < 8, fp64 (SK:553-629)
@@ -6530,7 +6544,7 @@ static int resolve_layout(int layout) {
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
       return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles), " \
-                     "4 (wave tiles) or 5 (k = 8 wave tiles without matrix cores)");                       \
+                     "4 (wave tiles) or 5 (k = 8 wave tiles on the matrix cores)");                       \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
@@ -6642,9 +6656,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
   if (k == 4 && layout != 4) return false;
   if (k == 8 && layout != 4 && layout != 5) return false;
-  // k = 8, layout 4: the matrix-core wave tiles (16-sample tiles); layout 5 (or rows not a multiple
-  // of 16): the VALU wave tiles (8-sample tiles)
-  const bool mf = k == 8 && layout == 4 && n_rows % 16 == 0;
+  // k = 8, layout 4: the VALU wave tiles (8-sample tiles); layout 5 (rows a multiple of 16): the
+  // matrix-core wave tiles (16-sample tiles; slower than layout 4 on the MI355X measured)
+  const bool mf = k == 8 && layout == 5 && n_rows % 16 == 0;
   const int tsw = mf ? 16 : 64 / k, wbw = tsw * k * 4;
   if (n_rows % tsw != 0) return false;
   const size_t l_wres = mf ? (size_t)wt::GeoMF8::L_WRES

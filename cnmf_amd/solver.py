@@ -445,8 +445,10 @@ class MUPlan:
         partial sums).  Call after the GPU has been busy for a while (the clock ramps up over the
         first ~35 ms of work).  Returns {layout: µs per iteration, the slowest rank's}.  No-op
         (empty dict) for non-persistent plans."""
-        if not self.persistent or self.k != 4 or self.xdt != _lib.F32:
-            return {}  # the layouts are alternatives for fp32 k = 4 only (k = 8: wave tiles)
+        if not self.persistent or self.k not in (4, 8) or self.xdt != _lib.F32:
+            return {}  # the layouts are alternatives for fp32 k = 4 and k = 8 only
+        if self.k == 8:  # k = 8: the VALU wave tiles (4) or the matrix-core wave tiles (5)
+            variants = (4, 5)
         W0, H0 = self.W.clone(), self.H64.clone()
         keep = self.layout
         times = {v: [] for v in variants}

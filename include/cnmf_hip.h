@@ -115,7 +115,9 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *   2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart (k = 4);
  *   3 = layout 1 with floating tiles: 80 % of the tiles stay with their workgroup (W resident), the
  *       rest is drawn from a pool every iteration (not bit-repeatable: the draw decides the order).
- * MUPlan.tune() times 4, 1 and 2 and keeps the fastest for its plan.  k = 8 has layout 4 only;
+ *   5 = k = 8 only: the wave tiles with both products on the matrix cores (v_mfma_f32_16x16x4_f32,
+ *       16-sample tiles; n_rows a multiple of 16, else layout 4);
+ * MUPlan.tune() times 4, 1 and 2 (k = 4) or 4 and 5 (k = 8) and keeps the fastest for its plan;
  * other values are CNMF_ERR_ARG. */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0

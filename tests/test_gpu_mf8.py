@@ -1,6 +1,6 @@
 """k = 8 on the matrix cores (mu_iter_mf8_kernel): the persistent wave-tile launch
-whose two products run on v_mfma_f32_16x16x4_f32 (layout 4, the default at k = 8) against the fp64
-oracle (north-star bar 1e-5), against the VALU wave tiles (layout 5: fp32 summation-order
+whose two products run on v_mfma_f32_16x16x4_f32 (layout 5) against the fp64
+oracle (north-star bar 1e-5), against the VALU wave tiles (layout 4, the default: fp32 summation-order
 agreement), bit-for-bit repeatable across split launches, W resident (LDS) and streamed, with the
 regularised update."""
 import numpy as np
@@ -12,7 +12,7 @@ from oracle import mu_ref
 pytestmark = pytest.mark.gpu
 
 
-def _plan(X, W0, H0, layout=0, **regs):
+def _plan(X, W0, H0, layout=5, **regs):
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1], **regs)
@@ -34,7 +34,7 @@ def test_mf8_matches_oracle_and_valu(n, iters):
     a.iterate(iters)
     a.check_sync_error()
     assert a.counters_at_rest()
-    v = _plan(X, W0, H0, layout=5)
+    v = _plan(X, W0, H0, layout=0)
     assert "mu_iter_wt_kernel" in v.describe()
     v.iterate(iters)
     v.check_sync_error()

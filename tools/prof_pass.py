@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     ap.add_argument("--solver", default="mu", choices=["mu", "als"],
                     help="als: the persistent constrained ALS (sum_to_one 1, smoothness 0.5)")
+    ap.add_argument("--layout", type=int, default=0, help="the persistent launch's layout (include/cnmf_hip.h)")
     a = ap.parse_args()
     import torch
     from cnmf_amd.solver import MUPlan
@@ -32,6 +33,7 @@ def main():
         plan = ALSPlan(Xd, a.k, sum_to_one=1.0, smoothness=0.5)
     else:
         plan = MUPlan(Xd, a.k)
+        plan.layout = a.layout
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     plan.iterate(a.iters)

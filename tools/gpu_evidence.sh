@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-end evidence on one MI355X: the GPU test suite, smoke, the default bench line and the
+# Evidence on one MI355X (usage: tools/gpu_evidence.sh <dir under gpurun_out>): the GPU test suite, smoke, the default bench line and the
 # driver's short form, HBM-traffic PMC passes and kernel-trace stats of the bench, every BASELINE
 # config's bench line, the headline shape at the per-GPU shard sizes of the strong-scaling runs
 # (N = 2, 4, 8 of V = 1e6), and kernel-trace stats of the cfg5 ALS bench.  Each GPU step has its
 # own time limit; the chain stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-D=gpurun_out/final2
+D=gpurun_out/${1:-evidence}
 mkdir -p $D/pmc
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 T="python -u -m pytest -x -v -p no:cacheprovider --timeout 180 --timeout-method thread"
@@ -23,6 +23,7 @@ $B --solver als --steps 200 --warmup 50 --cpu-seconds 10 > $D/bench_cfg5.json 2>
 $B --features 300 --k 16 --dtype bf16 --steps 100 --warmup 5 --no-cpu > $D/bench_cfg4.json 2> $D/bench_cfg4.err &&
 timeout -k 10 400 python -u bench.py --rows 10000000 --k 8 --steps 200 --warmup 200 --no-cpu > $D/bench_cfg3.json 2> $D/bench_cfg3.err &&
 $B --rows 1250000 --k 8 --steps 500 --warmup 500 --no-cpu > $D/bench_cfg3shard.json 2> $D/bench_cfg3shard.err &&
+$B --tol 1e-4 --steps 500 --warmup 500 --no-cpu > $D/bench_tol.json 2> $D/bench_tol.err &&
 $B --weighted --steps 200 --warmup 50 --no-cpu > $D/bench_weighted.json 2> $D/bench_weighted.err &&
 $B --rows 499968 --steps 500 --warmup 500 --no-cpu > $D/bench_shard_n2.json 2> $D/bench_shard_n2.err &&
 $B --rows 249984 --steps 500 --warmup 500 --no-cpu > $D/bench_shard_n4.json 2> $D/bench_shard_n4.err &&

@@ -77,6 +77,8 @@ def parse():
                         "tens of ms of work; the state is restored, the timed K steps are unchanged)")
     p.add_argument("--no-tune", action="store_true",
                    help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
+    p.add_argument("--layout", type=int, default=0,
+                   help="> 0: run this persistent layout (include/cnmf_hip.h) instead of tuning")
     p.add_argument("--tol", type=float, default=0.0,
                    help="> 0: the timed fit runs sklearn's tolerance test (SK:872-884) on the device "
                         "(cnmf_mu_fit_tol: ONE launch, the error every 10 iterations inside it); value = "
@@ -383,7 +385,9 @@ def main():
     # choice is collective (MUPlan.tune max-reduces the times over the ranks): every rank launches
     # the same layout
     tuned = {}
-    if args.solver == "mu" and plan.persistent and not args.no_tune and not args.weighted:
+    if args.layout > 0 and args.solver == "mu" and not args.weighted:
+        plan.layout = args.layout
+    elif args.solver == "mu" and plan.persistent and not args.no_tune and not args.weighted:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
     layout = plan.describe() if plan.persistent else None

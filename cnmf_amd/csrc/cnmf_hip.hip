@@ -2109,6 +2109,11 @@ __device__ unsigned long long g_tl_pub[TL_IT];
 __device__ unsigned long long g_tl_x[TL_IT * 4];  // MULTI exchange: start, stored, flags seen, summed
 __device__ unsigned long long g_tl_start[TL_WG];
 __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits), HW_REG_XCC_ID
+__device__ unsigned long long g_tl_rs[TL_IT * TL_WG * 3];  // layout 6: rows seen, columns published, AB seen
+#define TL_RS(it_, slot_)                                                                        \
+  do {                                                                                          \
+    if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_rs[((it_) * TL_WG + b) * 3 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #define TL(it_, slot_)                                                                          \
   do {                                                                                          \
     if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
@@ -2128,6 +2133,7 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
   } while (0)
 #else
 #define TL(it_, slot_) do {} while (0)
+#define TL_RS(it_, slot_) do {} while (0)
 #define TL_PUB(it_) do {} while (0)
 #define TL_X(it_, slot_) do {} while (0)
 #define TL_START do {} while (0)
@@ -2184,6 +2190,7 @@ __device__ __forceinline__ void xchg_allreduce_ab(uint64_t* xctl, double* AB, do
     uint64_t w[QB][4];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
+      const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // same batch
   #pragma unroll
       for (int j = 0; j < QB; ++j) {
         const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
@@ -2207,7 +2214,7 @@ __device__ __forceinline__ void xchg_allreduce_ab(uint64_t* xctl, double* AB, do
         __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (ev != 0u) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TIMEOUT) {
         __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -2549,8 +2556,10 @@ __global__ __launch_bounds__(NT * TEAMS, TEAMS == 2 ? 1 : (PD == 1 ? 3 : 2)) voi
       if (tid == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        while (true) {  // the flag and the error word in one batch: one round trip per round
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+          if (ev != 0u) {
             sFlag[2] = 0;
             break;
           }
@@ -2651,7 +2660,10 @@ struct Geo {
   static constexpr int L_HHT = L_HT + NL * NQ * KK * 4;                 // HHᵀ fp64 [K][K]
   static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 8 ints
   static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] wave loss sums, init, prev
-  static constexpr int L_WRES = (L_LOSS + 8 * 8 + 15) / 16 * 16;        // [NWV][nbt_max][WBW]
+  // RS: one fp64 value per (column, row) pair of the workgroup's columns (≤ NOUT + 1 + NT - 1)
+  static constexpr int RSV = NOUT + 1 + 256;
+  static constexpr int L_RSV = (L_LOSS + 8 * 8 + 15) / 16 * 16;
+  static constexpr int L_WRES = L_RSV + RSV * 8;                        // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
   static_assert(OVR >= 0 && PADB / 4 <= 64, "one zero float per lane covers the overrun");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
@@ -2805,6 +2817,7 @@ __device__ __forceinline__ void xchg_allreduce_n(uint64_t* xctl, double* AB, dou
     uint64_t w[QB][2 * U];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
+      const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // same batch
 #pragma unroll
       for (int j = 0; j < QB; ++j) {
         const uint64_t* src = mine + (size_t)min(q0 + j, xworld - 1) * slot;
@@ -2828,7 +2841,7 @@ __device__ __forceinline__ void xchg_allreduce_n(uint64_t* xctl, double* AB, dou
         __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
-      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (ev != 0u) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
         __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
@@ -2920,7 +2933,26 @@ __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, doub
 // workgroup leaves with the state after g iterations: H (not updated), W as it was before this
 // iteration's update — written to W itself in the loss iterations when W is resident in LDS, else to
 // the snapshot buffer (TC_WSNAP; the host copies it) — so n_iter = g as in sklearn.
-template <int KK, bool WRES, int PD, bool MULTI = false, bool TOL = false>
+//
+// RS (layout 6): the end of an iteration as ONE reduce-scatter over data-tagged granules instead of
+// the ticket tree (group combiners, top combiner, flag; 4.5 µs tail + 3.7 µs resume at cfg2,
+// DESIGN §3.0).  Every workgroup (1) publishes its fp64 row column-major, each value as two 8-byte
+// {tag = it + 1 : 32-bit half} granules (agent-scope stores: MI355X_MICROARCH.md R2 granules, the data
+// is the flag); (2) reduces its own columns c = b + G·j over the G rows in a fixed order (a poll of
+// its granules until every tag matches; rows in LDS; per column one wave's sequential + xor-tree
+// sum), (MULTI: exchanges those column sums with every rank, summed in rank order), and publishes the
+// sums as granules of AB; (3) polls all of AB, then applies the basis update itself.  Two hand-offs
+// per iteration, no counter, no flag.  A buffer is rewritten only after every reader of its previous
+// contents is done (a workgroup publishes row it + 1 after it has read all of AB(it), which needs
+// every column reduced, which needs every row read), so one buffer each suffices; the host zeroes
+// both before the launch (tags count within it).  The column sums' order is fixed (deterministic,
+// split launches bit-identical) but differs from the tree's, so layouts 4 and 6 agree to rounding.
+//
+// TAB (layout 7): the ticket tree of layout 4, but the top combiner publishes AB as data-tagged
+// granules (two per fp64 value, tag = it + 1) that every other workgroup polls directly: no flag,
+// and no separate AB load after it (one hand-off less in the resume); each workgroup takes the
+// tolerance decision itself from the same AB bits.
+template <int KK, bool WRES, int PD, bool MULTI = false, bool TOL = false, bool RS = false, bool TAB = false>
 __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   using namespace wt;
   using G_ = Geo<KK>;
@@ -3050,8 +3082,15 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // rewritten at the iteration's end), so that every set — the first PD too — has exactly PD stores
   // younger than it when its step waits (set q < PD: PD - q dummies, then the W stores of bodies
   // 0..q-1).  Counting PD stores that were never issued would let the set's last loads (the W tile)
-  // still be in flight when it is staged.
-  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
+  // still be in flight when it is staged.  (RS: into the stage buffer past AB's granules, a region
+  // nothing reads: the partial rows are handed off word by word, so a late dummy store must never be
+  // able to land on a published granule.)
+  // TAB: AB's granules in the stage buffer past the group rows (NG <= 16 for a grid of <= 256)
+  uint64_t* tabg = reinterpret_cast<uint64_t*>(a.groups + 32 * NOUTT);
+  float* dummy = RS ? reinterpret_cast<float*>(a.groups + 2 * NOUTT) + 64 * (gw & 63) + l
+                    : reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
+  if (RS && MULTI && t == 0)  // the launch's generation base (workgroup 0 advances it at its end)
+    sFlag[6] = (int)(uint32_t)__hip_atomic_load(a.xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
@@ -3077,6 +3116,258 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     stage(pfk);
     prefetch(pfk, gw + (int64_t)NW * nx_i);
     if (++nx_i == nbt) nx_i = 0;
+  };
+  // RS: the end of iteration `it` once the waves' sums are in `red` (the comment above the kernel).
+  // Returns true with the next iteration's basis in LDS, false when this workgroup leaves the launch
+  // (its last iteration, a tolerance stop, or a failed wait: then the error word is set).
+  // AB from its granules (two per fp64 value {tag : half}) into sAB, every value polled until both
+  // its granules carry the tag; returns 1 when the wait failed (timeout: the error word set here)
+  auto poll_ab = [&](const uint64_t* abg, uint32_t tag) -> int {
+    constexpr int UA = (NOUTT + NT - 1) / NT;  // AB values per thread
+    bool need[UA];
+#pragma unroll
+    for (int u = 0; u < UA; ++u) need[u] = t + NT * u < NOUTT;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // same batch
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < UA; ++u)
+        if (need[u]) {
+          const int o = t + NT * u;
+          const uint64_t lo = __hip_atomic_load(abg + 2 * o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const uint64_t hi = __hip_atomic_load(abg + 2 * o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag) {
+            sAB[o] = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
+            need[u] = false;
+          } else {
+            ok = false;
+          }
+        }
+      if (__all(ok)) return 0;
+      if (__builtin_amdgcn_readfirstlane(ev) != 0u) return 1;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 1;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto put_granules = [&](uint64_t* p, double v, uint32_t tag) {  // one fp64 value as {tag : half} x 2
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    __hip_atomic_store(p, ((uint64_t)tag << 32) | (u & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(p + 1, ((uint64_t)tag << 32) | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto rs_end = [&](int it, bool last_it, bool loss_it) -> bool {
+    constexpr int UR = (G_::RSV + NT - 1) / NT;  // (column, row) pairs per thread, at most
+    uint64_t* pg = reinterpret_cast<uint64_t*>(a.partials);  // [G][NOUTT][2] granules
+    uint64_t* abg = reinterpret_cast<uint64_t*>(a.groups);   // [NOUTT][2] granules
+    double* rsv = reinterpret_cast<double*>(smem + G_::L_RSV);
+    const uint32_t tag = (uint32_t)(it + 1);
+    auto put = [&](uint64_t* p, double v) { put_granules(p, v, tag); };
+    // (1) this workgroup's row: value o as granules pg[(b·NOUTT + o)·2 + {0, 1}] (coalesced stores)
+    for (int o = t; o < NOUTT; o += NT) {
+      double val;
+      if (TOL && o == NOUT) {
+        val = (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]);
+      } else {
+        const int j = o / V;
+        const int v = o - j * V;
+        const int ee = v < F ? v / NQ : j;
+        const int idx = v < F ? (v - NQ * ee) * KK + j : NQ * KK + (v - F);
+        const float* rr = red + ee * NACC + idx;
+        constexpr int WS = NL * NACC;  // wave stride
+        val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+      }
+      put(pg + ((size_t)b * NOUTT + o) * 2, val);
+    }
+    TL(it, 0);
+    // (2) this workgroup's columns c = b + G·j over the G rows: every (column, row) pair polled
+    // until both its granules carry the tag, the values to LDS
+    const int ncol = b < NOUTT ? (NOUTT - 1 - b) / G + 1 : 0;
+    const int npair = ncol * G;
+    int fail = 0;
+    {
+      size_t off[UR];
+      bool need[UR];
+#pragma unroll
+      for (int u = 0; u < UR; ++u) {
+        const int q = t + NT * u;
+        need[u] = q < npair;
+        const int j = q / G, r = q - (q / G) * G;
+        off[u] = ((size_t)r * NOUTT + (b + G * j)) * 2;
+      }
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (true) {
+        // the error word in the same batch as the granules (one round trip per round)
+        const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool ok = true;
+#pragma unroll
+        for (int u = 0; u < UR; ++u)
+          if (need[u]) {
+            const uint64_t lo = __hip_atomic_load(pg + off[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t hi = __hip_atomic_load(pg + off[u] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag) {
+              rsv[t + NT * u] = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
+              need[u] = false;
+            } else {
+              ok = false;
+            }
+          }
+        if (__all(ok)) break;
+        if (__builtin_amdgcn_readfirstlane(ev) != 0u) {
+          fail = 1;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          fail = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    if (__syncthreads_or(fail)) return false;
+    TL_RS(it, 0);
+    // (3) per column one wave: its lanes' rows in sequence, a fixed xor tree, lane 0's value (the
+    // same bits on every rank and run); MULTI: the ranks' sums for the column in rank order
+    for (int j = w; j < ncol; j += NWV) {
+      double sum = 0.0;
+      for (int r = l; r < G; r += 64) sum += rsv[j * G + r];
+      sum = __shfl(wave_sum(sum), 0, 64);
+      const int c = b + G * j;
+      if constexpr (MULTI) {
+        const int xrank = (int)__hip_atomic_load(a.xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int xworld = (int)__hip_atomic_load(a.xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t gen = (uint32_t)sFlag[6] + (uint32_t)it + 1u;
+        const size_t slot = 2 * (size_t)NOUTT;
+        const size_t par = (size_t)(gen & 1u) * xworld * slot;
+        const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+        const uint64_t xt = (uint64_t)(bad ? sl::XPOISON : gen) << 32;
+        const uint64_t u = (uint64_t)__double_as_longlong(sum);
+        if (l < xworld) {  // lane p -> rank p's buffer, slot xrank
+          uint64_t* peer = reinterpret_cast<uint64_t*>(
+              __hip_atomic_load(a.xctl + XC_PEERS + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          uint64_t* dst = peer + par + (size_t)xrank * slot + 2 * c;
+          __hip_atomic_store(dst, xt | (u & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(dst + 1, xt | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        const uint64_t* mine = reinterpret_cast<const uint64_t*>(
+            __hip_atomic_load(a.xctl + XC_PEERS + xrank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const uint64_t* src = mine + par + (size_t)min(l, xworld - 1) * slot + 2 * c;  // lane q: rank q's
+        uint64_t lo = 0, hi = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (true) {
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const uint32_t tl = (uint32_t)(lo >> 32), th = (uint32_t)(hi >> 32);
+          if (__all(tl == gen && th == gen)) break;
+          if (__any(tl == sl::XPOISON || th == sl::XPOISON)) {
+            __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fail = 1;
+            break;
+          }
+          if (__builtin_amdgcn_readfirstlane(ev) != 0u) {
+            fail = 1;
+            break;
+          }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+            __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            fail = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (fail) break;
+        const double vq = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
+        sum = 0.0;
+        for (int q = 0; q < xworld; ++q) sum += __shfl(vq, q, 64);  // rank order
+      }
+      if (l == 0) put(abg + 2 * c, sum);
+    }
+    if (__syncthreads_or(fail)) return false;
+    TL_RS(it, 1);
+    // (4) all of AB from its granules
+    fail = poll_ab(abg, tag);
+    if (__syncthreads_or(fail)) return false;
+    TL_RS(it, 2);
+    if (b == 0) TL_PUB(it);
+    // (5) the tolerance test (SK:872-884) on the state after it0 + it iterations: every workgroup
+    // decides from the same AB bits; workgroup 0 keeps the host's record
+    if (TOL && loss_it) {
+      if (t == 0) {
+        const int gi = it0 + it;
+        const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+        int stop = 0;
+        if (b == 0) {
+          const int slot = gi / 10;
+          if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
+          st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
+        }
+        if (gi == 0) {
+          sLoss[4] = sLoss[5] = errv;
+          if (b == 0) {
+            st_sc1(a.tolctl + TC_INIT, errv);
+            st_sc1(a.tolctl + TC_PREV, errv);
+          }
+        } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
+          stop = 1;
+        } else {
+          sLoss[5] = errv;
+          if (b == 0) st_sc1(a.tolctl + TC_PREV, errv);
+        }
+        sFlag[3] = stop;
+      }
+      __syncthreads();
+      if (sFlag[3]) {  // stopped: the state after it0 + it iterations (W already in place, H = sH)
+        if (b != 0) return false;
+        for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+        for (int o = t; o < F * KK; o += NT) {
+          const int f = o / KK;
+          const int j = o - f * KK;
+          a.Ht[o] = sH[j * F + f];
+        }
+        if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
+        if (t == 0) {
+          st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
+          st_sc1(a.tolctl + TC_STOPPED, 1.0);
+          st_sc1(a.tolctl + TC_IN_SNAP, WRES ? 0.0 : 1.0);
+          if (MULTI)
+            __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return false;
+      }
+    }
+    if (last_it) {
+      if (WRES)  // this wave's W back to HBM, once per launch
+        for (int c = l; c < nbt * (WBW / 16); c += 64) {
+          const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+          *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+              *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
+        }
+      if (b != 0) return false;
+      for (int o = t; o < NOUTT; o += NT) a.AB[o] = sAB[o];  // the last iteration's accumulators
+      if (a.apply_last) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < F * KK; o += NT) {
+        const int f = o / KK;
+        const int j = o - f * KK;
+        a.Ht[o] = sH[j * F + f];
+      }
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
+      if (t == 0) {
+        if (TOL) {
+          st_sc1(a.tolctl + TC_DONE, (double)(it0 + a.n_iter));
+          st_sc1(a.tolctl + TC_STOPPED, 0.0);
+        }
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return false;
+    }
+    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+    return true;
   };
   auto body = [&]() {
     const int it = cur_it, i = cur_i;
@@ -3253,6 +3544,15 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       lossacc = 0.0;
     }
     __syncthreads();
+    if constexpr (RS) {
+      if (!rs_end(it, last_it, loss_it)) {
+        alive = false;
+        return;
+      }
+      load_basis();
+      TL(it, 1);
+      return;
+    }
     // the workgroup's fp64 row [K][V] (+ the loss): the four waves' sums in wave order (deterministic)
     {
       double* prow = a.partials + (size_t)b * NOUTT;
@@ -3296,6 +3596,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
+        if (TAB && must_wait)  // AB as granules for the others (this thread's own outputs of the sums)
+          for (int o = t; o < NOUTT; o += NT) put_granules(tabg + 2 * o, sAB[o], (uint32_t)(it + 1));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // (after the barrier: the summed loss sAB[NOUT] was written by another thread)
@@ -3317,20 +3619,42 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
           }
         }
         if (TOL && loss_it) __syncthreads();  // sFlag[3] (the decision) for the whole workgroup
-        if (t == 0 && must_wait)
+        if (!TAB && t == 0 && must_wait)
           __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         TL_PUB(it);
       }
     }
     const bool top = sFlag[1] != 0;
-    if (!top && must_wait) {
+    if (TAB && !top && must_wait) {  // AB straight from the top's granules
+      if (__syncthreads_or(poll_ab(tabg, (uint32_t)(it + 1)))) {
+        alive = false;
+        return;
+      }
+      if (TOL && loss_it) {  // the top's decision, taken here from the same AB bits and state
+        if (t == 0) {
+          const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+          int stop = 0;
+          if (it0 + it == 0)
+            sLoss[4] = sLoss[5] = errv;
+          else if ((sLoss[5] - errv) / sLoss[4] < tolv)
+            stop = 1;
+          else
+            sLoss[5] = errv;
+          sFlag[3] = stop;
+        }
+        __syncthreads();
+      }
+    } else if (!top && must_wait) {
       if (t == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t f;
-        while (((f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~FLAG_STOP) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        while (true) {  // the flag and the error word in one batch: one round trip per round
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((f & ~FLAG_STOP) >= want) break;
+          if (ev != 0u) {
             sFlag[2] = 0;
             break;
           }
@@ -3404,7 +3728,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       return;
     }
-    if (!top) {
+    if (!TAB && !top) {
       for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
       if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
@@ -3826,8 +4150,11 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t f;
-        while (((f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & ~FLAG_STOP) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        while (true) {  // the flag and the error word in one batch: one round trip per round
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((f & ~FLAG_STOP) >= want) break;
+          if (ev != 0u) {
             sFlag[2] = 0;
             break;
           }
@@ -5685,8 +6012,10 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
       if (t == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        while (true) {  // the flag and the error word in one batch: one round trip per round
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+          if (ev != 0u) {
             sFlag[2] = 0;
             break;
           }
@@ -6070,8 +6399,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       if (t == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-          if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        while (true) {  // the flag and the error word in one batch: one round trip per round
+          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+          if (ev != 0u) {
             sFlag[2] = 0;
             break;
           }
@@ -6455,6 +6786,10 @@ int cnmf_debug_hstep(unsigned long long* host_out) {  // [64 calls][4 rows][BPP 
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hs), sizeof(unsigned long long) * 64 * 4 * 2));
   return CNMF_OK;
 }
+int cnmf_debug_rs_timeline(unsigned long long* host_out) {  // [TL_IT][TL_WG][3]
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_rs), sizeof(unsigned long long) * TL_IT * TL_WG * 3));
+  return CNMF_OK;
+}
 int cnmf_debug_xtimeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
   return CNMF_OK;
@@ -6537,14 +6872,15 @@ static int default_layout() {
 }
 static int resolve_layout(int layout) {
   if (layout == 0) return default_layout();
-  return (layout >= 1 && layout <= 5) ? layout : -1;
+  return (layout >= 1 && layout <= 7) ? layout : -1;
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
       return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles), " \
-                     "4 (wave tiles) or 5 (k = 8 wave tiles on the matrix cores)");                       \
+                     "4 (wave tiles), 5 (k = 8 wave tiles on the matrix cores), 6 (wave tiles, reduce-scatter "  \
+                     "end of iteration) or 7 (wave tiles, AB as tagged granules)");                       \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
@@ -6610,7 +6946,17 @@ static int wt_pd(int k, bool wres, bool multi) {
 }
 extern "C++" {
 template <int KK, bool WRES>
-static PassFn wt_fn_k(int pd, bool multi, bool tol) {
+static PassFn wt_fn_k(int pd, bool multi, bool tol, bool rs, bool tab) {
+  if (tab)  // layout 7: the ticket tree with AB published as tagged granules, PD = 3
+    return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true, false, true>)
+                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true, false, true>))
+               : (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, false, false, true>)
+                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, false, false, true>));
+  if (rs)  // layout 6: the reduce-scatter end of iteration, PD = 3
+    return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true, true>)
+                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true, true>))
+               : (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, false, true>)
+                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, false, true>));
   if (tol)  // the device tolerance test: PD = 3
     return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true>)
                  : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true>);
@@ -6631,10 +6977,10 @@ static PassFn mf8_fn(bool wres, bool multi, bool tol) {
              : (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, true, false>)
                       : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, false>));
 }
-static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false) {
-  const int pd = tol ? 3 : wt_pd(k, wres, multi);
-  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol) : wt_fn_k<4, false>(pd, multi, tol);
-  return wres ? wt_fn_k<8, true>(pd, multi, tol) : wt_fn_k<8, false>(pd, multi, tol);
+static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false, bool rs = false, bool tab = false) {
+  const int pd = (tol || rs || tab) ? 3 : wt_pd(k, wres, multi);
+  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol, rs, tab) : wt_fn_k<4, false>(pd, multi, tol, rs, tab);
+  return wres ? wt_fn_k<8, true>(pd, multi, tol, rs, tab) : wt_fn_k<8, false>(pd, multi, tol, rs, tab);
 }
 static int device_cus() {
   static int cus[64] = {0};
@@ -6648,14 +6994,18 @@ struct WtLaunch {
   int64_t G, n_tiles;
   size_t lds;
   bool mf;  // k = 8 on the matrix cores (mu_iter_mf8_kernel)
+  bool rs;  // layout 6: the reduce-scatter end of iteration (partials hold 2·G rows of granules)
+  int k;
+  bool tab;  // layout 7: the ticket tree, AB published as tagged granules (stage rows 32..)
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
 static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, WtLaunch* out,
                     bool tol = false) {
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
-  if (k == 4 && layout != 4) return false;
-  if (k == 8 && layout != 4 && layout != 5) return false;
+  if (k == 4 && layout != 4 && layout != 6 && layout != 7) return false;
+  if (k == 8 && layout != 4 && layout != 5 && layout != 6 && layout != 7) return false;
+  const bool rs = layout == 6, tab = layout == 7;
   // k = 8, layout 4: the VALU wave tiles (8-sample tiles); layout 5 (rows a multiple of 16): the
   // matrix-core wave tiles (16-sample tiles; slower than layout 4 on the MI355X measured)
   const bool mf = k == 8 && layout == 5 && n_rows % 16 == 0;
@@ -6666,7 +7016,7 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
   const int ncu = device_cus();
   const int64_t n_tiles = n_rows / tsw;
   for (int wres = 1; wres >= 0; --wres) {
-    const int pd = tol ? 3 : wt_pd(k, wres != 0, multi);
+    const int pd = (tol || rs || tab) ? 3 : wt_pd(k, wres != 0, multi);
     // tiles per wave: > PD (the first prefetches), >= 2·PD + 1 when W is streamed (re-load hazard)
     const int min_nbt = wres ? pd + 1 : 2 * pd + 1;
     const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
@@ -6674,9 +7024,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
     if (lds > kMaxLds) continue;
-    const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol);
+    const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol, rs, tab);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
-    *out = WtLaunch{fn, G, n_tiles, lds, mf};
+    *out = WtLaunch{fn, G, n_tiles, lds, mf, rs, k, tab};
     return true;
   }
   return false;
@@ -6804,10 +7154,19 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
                         n_features, k, sum_to_one, smoothness, xctl, events, n_events, stream);
 }
 
+// the wave-tile launch of this shape and layout that the buffers can serve: layout 6 keeps its
+// granules in the partials (2·G rows of k(F+k)+1 doubles, column-major) — with fewer rows the
+// ticket tree of layout 4 serves the shape
+static bool wt_plan_n(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, int64_t n_parts,
+                      WtLaunch* L, bool tol = false) {
+  if (wt_plan(n_rows, x_dtype, F, k, multi, layout, L, tol) && L->G <= n_parts && (!L->rs || 2 * L->G + 2 <= n_parts))
+    return true;
+  return layout == 6 && wt_plan(n_rows, x_dtype, F, k, multi, 4, L, tol) && L->G <= n_parts;
+}
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
                      double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
                      double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl,
-                     double* tolctl = nullptr) {
+                     double* tolctl = nullptr, void* const* events = nullptr, int n_events = 0) {
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
   PersistArgs pa;
@@ -6833,7 +7192,15 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.xctl = xctl;
   pa.tolctl = tolctl;
   void* args[] = {&pa};
+  const size_t noutt = (size_t)L.k * (wt::F + L.k) + (tolctl ? 1 : 0);
+  if (L.rs) {  // every granule's tag back to 0 (tags count iterations within the launch)
+    HIP_CHECK(hipMemsetAsync(partials, 0, 2 * (size_t)L.G * noutt * sizeof(double), s));
+    HIP_CHECK(hipMemsetAsync(stage, 0, 2 * noutt * sizeof(double), s));
+  }
+  if (L.tab) HIP_CHECK(hipMemsetAsync(stage + 32 * noutt, 0, 2 * noutt * sizeof(double), s));
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), s));
   HIP_CHECK(hipLaunchKernel(L.fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, s));
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), s));
   return CNMF_OK;
 }
 
@@ -6868,8 +7235,11 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
     else
       snprintf(out, (size_t)len,
                "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
-               "(%lld workgroups), no barrier inside an iteration",
-               k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
+               "(%lld workgroups), no barrier inside an iteration; %s",
+               k, wres ? "resident in LDS" : "streamed with X", L.rs ? 3 : wt_pd(k, wres, false), 64 / k, (long long)L.G,
+               L.rs ? "end of iteration: one reduce-scatter over tagged granules (layout 6)"
+                    : (L.tab ? "end of iteration: ticket tree, AB as tagged granules (layout 7)"
+                             : "end of iteration: ticket tree + flag (layout 4)"));
     return 1;
   }
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
@@ -7070,7 +7440,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
   {  // one wave-tile launch with n_iter = 1: the multi-iteration launch's layout, so the RCCL path
      // and the in-launch exchange sum the same partials; only tickets, no waits
     WtLaunch L;
-    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts)
+    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, layout >= 6 ? 4 : layout, &L) && L.G <= n_parts)
       return launch_wt(L, 1, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
                        apply_first, 0, hs, nullptr);
   }
@@ -7138,15 +7508,11 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
   RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts) {
+    if (wt_plan_n(n_rows, x_dtype, n_features, k, false, layout, n_parts, &L)) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
-      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
-      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
-                               l2_H, 0, 1, hs, nullptr);
-      if (st) return st;
-      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
-      return CNMF_OK;
+      return launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H, 0, 1,
+                       hs, nullptr, nullptr, events, n_events);
     }
   }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
@@ -7210,15 +7576,11 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
   RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan(n_rows, x_dtype, n_features, k, true, layout, &L) && L.G <= n_parts) {
+    if (wt_plan_n(n_rows, x_dtype, n_features, k, true, layout, n_parts, &L)) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
-      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
-      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
-                               l2_H, 0, 1, hs, xctl);
-      if (st) return st;
-      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
-      return CNMF_OK;
+      return launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H, 0, 1,
+                       hs, xctl, nullptr, events, n_events);
     }
   }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k, true);
@@ -7248,18 +7610,17 @@ int cnmf_mu_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H
   RESOLVE_LAYOUT(layout);
   if (max_iter <= 0) return set_err(CNMF_ERR_ARG, "max_iter must be >= 1");
   WtLaunch L;
-  if (!wt_plan(n_rows, x_dtype, n_features, k, xctl != nullptr, layout, &L, true))
+  if (!wt_plan_n(n_rows, x_dtype, n_features, k, xctl != nullptr, layout, n_parts < 0 ? 0 : n_parts, &L, true) &&
+      !wt_plan(n_rows, x_dtype, n_features, k, xctl != nullptr, layout == 6 ? 4 : layout, &L, true))
     return set_err(CNMF_ERR_UNSUPPORTED, "the device tolerance test serves the wave-tile launch (fp32 X, F = 81, "
-                   "k = 4 or 8, layout 4; n_rows=%lld F=%d k=%d layout=%d)", (long long)n_rows, n_features, k, layout);
+                   "k = 4 or 8, layout 4 or 6; n_rows=%lld F=%d k=%d layout=%d)", (long long)n_rows, n_features, k, layout);
   if (L.G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
                                     (long long)n_parts, (long long)L.G);
   if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !tolctl)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
-  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   const int st = launch_wt(L, max_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
-                           0, 1, hs, xctl, tolctl);
+                           0, 1, hs, xctl, tolctl, events, n_events);
   if (st) return st;
-  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   // the iteration flag may still hold the last (or the stopping) iteration: cleared in stream order
   HIP_CHECK(hipMemsetAsync(counter + CNT_FLAG, 0, sizeof(uint32_t), hs));
   return CNMF_OK;

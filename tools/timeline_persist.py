@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--solver", default="mu", choices=["mu", "als", "wmu"],
                     help="als: the persistent constrained ALS (sum_to_one 1, smoothness 0.5); wmu: the "
                          "persistent weighted MU (30 %% zero weights)")
+    ap.add_argument("--layout", type=int, default=0, help="the plan's persistent layout (0 = default)")
     ap.add_argument("--exchange", action="store_true",
                     help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
     a = ap.parse_args()
@@ -62,6 +63,8 @@ def main():
         plan = MUPlan(torch.from_numpy(X).cuda(), a.k, group=group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
+    if a.layout and hasattr(plan, "layout"):
+        plan.layout = a.layout
     if a.exchange:
         plan.enable_exchange()
     assert plan.persistent
@@ -133,6 +136,21 @@ def main():
     summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
                     "us_per_iter": round(launch_us / a.iters, 2),
                     "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})
+    if a.layout == 6:  # the reduce-scatter end: per iteration, from the last arrival
+        fr = lib.cnmf_debug_rs_timeline
+        fr.argtypes = [ctypes.c_void_p]
+        fr.restype = ctypes.c_int
+        rb = np.zeros(TL_IT * TL_WG * 3, dtype=np.uint64)
+        _lib.check(fr(rb.ctypes.data), "rs timeline")
+        rs = rb.reshape(TL_IT, TL_WG, 3).astype(np.int64)[1:n - 1, :g]
+        last = arr[1:n - 1].max(axis=1)[:, None]
+        ready = res[1:n - 1]
+        def q(v):
+            return [round(float(np.median(np.median(v, axis=1))) * 10 / 1e3, 2),
+                    round(float(np.median(v.max(axis=1))) * 10 / 1e3, 2)]
+        summary["rs_from_last_arrival_us_median_max"] = {
+            "rows_seen": q(rs[:, :, 0] - last), "columns_published": q(rs[:, :, 1] - last),
+            "ab_seen": q(rs[:, :, 2] - last), "basis_ready": q(ready - last)}
     if a.exchange:
         fx = lib.cnmf_debug_xtimeline
         fx.argtypes = [ctypes.c_void_p]

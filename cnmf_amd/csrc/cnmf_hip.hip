@@ -1098,6 +1098,318 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
 }
 
 // ------------------------------------------------------------------------------------------------
+// mu_pass_bfw_kernel — the bf16 matrix-core pass of cfg4 (bf16 X, 9 <= k <= 16, F <= 320) as
+// barrier-free WAVE tiles (mu_iter_wt_kernel's layout).
+//
+// mu_pass_bf16_mfma_kernel above shares each 64-sample tile among the workgroup's four waves and
+// synchronises them three times per tile (staging, W'ᵀ hand-off, end of tile): at 2 waves per SIMD
+// it ran latency-bound at 0.49 of HBM with 17 % MFMA busy and 16 % of cycles in LDS bank conflicts
+// (profiles/r02/pmc_cfg/SUMMARY.md).  Here every wave owns a quarter of each of its workgroup's
+// 64-sample tiles (16 samples, 9600 B of X at F = 300) and runs the whole update on it alone:
+//   * prefetch: PD = 2 wave tiles in flight, X (10 x 16 B per lane) and W (one 16-byte chunk) loaded
+//     by inline asm into AGPRs and waited for with exact counted `s_waitcnt vmcnt` (every body issues
+//     exactly four stores, invalid lanes to a dummy word in this workgroup's partial row), staged into
+//     the wave's own LDS slot: no barrier anywhere in the loop;
+//   * phase 1  num[s][n] = Σ_f x[s][f]·h[n][f] on v_mfma_f32_16x16x32_bf16 (A = X rows, B = the three
+//     bf16 terms of H, one fp32 chain per K-step folded into fp64) — as the 64-sample kernel;
+//   * phase 2  den = w·HHᵀ on v_mfma_f64_16x16x4_f64, the fp64 update (SK:553-629); the lane's four
+//     new w'[4g + r][li] are exactly the A operand of phase 3 (row m = li, k = samples 4g..4g+3), so
+//     W' never goes through LDS;
+//   * phase 3  A[m][f] += Σ_s w'[s][m]·x[s][f] on v_mfma_f32_16x16x16_bf16 (K = the tile's 16 samples;
+//     B = X columns by ds_read_b64_tr_b16; w' in three bf16 terms, so every product is exact in fp32);
+//     B[m][n] += Σ_s w'[s][m]·w'[s][n] on v_mfma_f32_16x16x4_f32.  The fp32 MFMA accumulators chain
+//     over the wave's tiles (≈ 61 at cfg4: the per-lane fp32 accumulation of mu_iter_wt_kernel);
+//   * end of launch: the four waves' accumulators summed in LDS in the fixed order (w0 + w2) + (w1 + w3)
+//     in fp64, one partial row per workgroup (mu_pass_bf16_mfma_kernel's row layout).
+// Full 64-sample tiles only (the host runs a ragged tail on one workgroup of the 64-sample kernel).
+// ------------------------------------------------------------------------------------------------
+namespace bw {
+constexpr int TSW = 16;       // samples per wave tile
+constexpr int PFX = 10;       // 16-byte X loads per lane per wave tile (2F chunks, F <= 320)
+constexpr int PFS = PFX + 1;  // + the wave tile's W (64k bytes: one chunk per lane, k <= 16)
+constexpr int PD = 2;         // wave tiles in flight per wave
+constexpr int NBX = 20;       // 16-feature blocks (F <= 320)
+constexpr int NSTB = 4;       // global stores per body (the lane's four w')
+struct Lds {
+  int hs, hrow, hht, slot, xbytes, slotb, red, total;
+};
+__host__ __device__ inline Lds lds(int F) {
+  Lds L;
+  L.hrow = (32 * bm::ksteps(F) + 8) * 2;                // H split rows (bm's conflict-free stride)
+  L.hs = 0;
+  L.hht = L.hs + 3 * bm::KP * L.hrow;
+  L.xbytes = (int)align16((size_t)TSW * F * 2 + 64);   // + 64 zero bytes for the reads past the last row
+  L.slotb = L.xbytes + TSW * 16 * 4;                   // + the wave tile's W [16][k <= 16] fp32
+  L.slot = (int)align16((size_t)L.hht + 16 * 16 * 8);
+  L.red = 2 * (NBX + 1) * 4 * 64 * 8;                  // end of launch: two waves' fp64 sums
+  const int loop = L.slot + 4 * L.slotb;
+  L.total = loop > L.red ? loop : L.red;
+  return L;
+}
+__device__ __forceinline__ void ld16(u32x4& r, const unsigned char* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off nt" : "=a"(r) : "v"(p) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_set(u32x4 (&pf)[PFS]) {
+  static_assert(PFS == 11, "one operand per prefetch register");
+  asm volatile("s_waitcnt vmcnt(%11)"
+               : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5]), "+a"(pf[6]),
+                 "+a"(pf[7]), "+a"(pf[8]), "+a"(pf[9]), "+a"(pf[10])
+               : "n"(N) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void st16(unsigned addr, const u32x4& v) {
+  asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
+}
+template <int U>
+__device__ __forceinline__ void stage_x(unsigned addr, const u32x4* pf, int l, int nch) {
+  if (l + 64 * U < nch) st16<1024 * U>(addr, pf[U]);
+  if constexpr (U + 1 < PFX) stage_x<U + 1>(addr, pf, l, nch);
+}
+}  // namespace bw
+
+// KSC > 0: K-steps (and 2·KSC feature blocks) and KC components at compile time (cfg4: KSC = 10,
+// F in 289..320, KC = 16): fully unrolled, branch-free phases the scheduler can interleave (with
+// runtime bounds every K-step and feature block was its own basic block: phases 1 and 3 ran as
+// dependent chains, 2647 and 2263 cycles per wave tile, profiles/r03/bfw/); KSC = 0: runtime F, k.
+template <int KSC, int KC>
+__global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __restrict__ X, float* __restrict__ W,
+                                                            const double* __restrict__ Ht,
+                                                            const double* __restrict__ HHt,
+                                                            double* __restrict__ partials, int64_t n_rows, int F,
+                                                            int k, double l1, double l2, int flags,
+                                                            int64_t n_tiles) {
+  using namespace bw;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const Lds L = lds(F);
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = l >> 4, li = l & 15;
+  const int KS = KSC ? KSC : bm::ksteps(F);
+  const int NB = KSC ? 2 * KSC : (F + 15) / 16;  // KSC: the last blocks past F read finite pads / rows
+  if (KC) k = KC;
+  const int nchx = 2 * F, nchw = 4 * k;  // 16-byte chunks of a wave tile's X and W
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+  unsigned char* xs = smem + L.slot + w * L.slotb;  // this wave's X tile [16][F] bf16 (+ zero pad)
+  const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);  // its W tile [16][k] fp32
+
+  // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
+  for (int e = t; e < bm::KP * 32 * KS; e += NT) {
+    const int n = e / (32 * KS);
+    const int f = e - n * 32 * KS;
+    const double h = (n < k && f < F) ? Ht[(size_t)f * bm::KP + n] : 0.0;
+    const uint16_t h1 = bm::bf16_rn((float)h);
+    const double r1 = h - (double)bm::bf16_f(h1);
+    const uint16_t h2 = bm::bf16_rn((float)r1);
+    const double r2 = r1 - (double)bm::bf16_f(h2);
+    const uint16_t h3 = bm::bf16_rn((float)r2);
+    uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;
+    row[0] = h1;
+    row[bm::KP * L.hrow / 2] = h2;
+    row[2 * bm::KP * L.hrow / 2] = h3;
+  }
+  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
+  for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = HHt[e];
+  if (l < 16) reinterpret_cast<uint32_t*>(xs + TSW * F * 2)[l] = 0u;  // the wave's zero pad
+  __syncthreads();
+  double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li]
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * bm::KP + li];
+
+  // ---- this wave's tiles: rows [64·(blockIdx + G·i) + 16w, +16), i < ntw (full 64-sample tiles)
+  const int64_t G = gridDim.x;
+  const int ntw = (int)((n_tiles - blockIdx.x + G - 1) / G);
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(X);
+  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(W);
+  auto row0 = [&](int i) -> int64_t {  // first row of wave tile i (past the last: row 16w of tile 0)
+    return 64 * (i < ntw ? (int64_t)blockIdx.x + G * i : (int64_t)blockIdx.x) + 16 * w;
+  };
+  auto prefetch = [&](u32x4 (&pf)[PFS], int i) {
+    const int64_t r0 = row0(i);
+    const unsigned char* xsrc = Xb + (size_t)r0 * F * 2;
+#pragma unroll
+    for (int u = 0; u < PFX; ++u) ld16(pf[u], xsrc + 16 * (l + 64 * u < nchx ? l + 64 * u : l));
+    ld16(pf[PFX], Wb + (size_t)r0 * k * 4 + 16 * (l < nchw ? l : 0));
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS]) {
+    stage_x<0>((unsigned)(uintptr_t)(xs + 16 * l), pf, l, nchx);
+    if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * l), pf[PFX]);
+  };
+
+  // accumulators: phase 3's fp32 MFMA chains over the wave's tiles (in AGPRs: no VALU touches
+  // them before the end of the launch, so the 20 block chains run interleaved)
+  f32x4 cacc[NBX], bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nb = 0; nb < NBX; ++nb) cacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // invalid lanes' stores land in this workgroup's partial row (rewritten at the end of the launch;
+  // the host guarantees k(F+k) >= 512 doubles): every body issues exactly NSTB stores per lane
+  float* dummy = reinterpret_cast<float*>(partials + (size_t)blockIdx.x * k * (F + k)) + 64 * w + l;
+  STAMP_DECL
+
+  auto body = [&](int i) {
+    const int64_t r0 = row0(i);
+    // phase 1: num for samples 4g + r, component li (16x16x32 bf16 against H's three terms)
+    double num64[4] = {0.0, 0.0, 0.0, 0.0};
+    {
+      const unsigned char* xa = xs + ((size_t)li * F + 8 * g) * 2;
+      const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
+#pragma unroll
+      for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
+        if (!KSC && ks >= KS) break;
+        const uint64_t a0 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks);
+        const uint64_t a1 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks + 8);
+        s16x8 a;
+        a.s0123 = __builtin_bit_cast(s16x4, a0);
+        a.s4567 = __builtin_bit_cast(s16x4, a1);
+        const s16x8 b1 = *reinterpret_cast<const s16x8*>(hb + 64 * ks);
+        const s16x8 b2 = *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks);
+        const s16x8 b3 = *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks);
+        const bf16x8 av = __builtin_bit_cast(bf16x8, a);
+        f32x4 num = f32x4{0.f, 0.f, 0.f, 0.f};
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b3), num, 0, 0, 0);
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b2), num, 0, 0, 0);
+        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b1), num, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) num64[r] += (double)num[r];
+      }
+    }
+    STAMP(3);  // 3: phase 1
+    // phase 2: den = w·HHᵀ (f64 MFMA; A row ρ = li carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is
+    // sample 4g + r), then w' = w·num/den (SK:553-629) for (s = 4g + r, n = li)
+    f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int sa = 4 * (li & 3) + (li >> 2);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int m = 4 * kk + g;
+      const double av = m < k ? (double)wso[sa * k + m] : 0.0;
+      den = __builtin_amdgcn_mfma_f64_16x16x4f64(av, hhb[kk], den, 0, 0, 0);
+    }
+    float wr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = 4 * g + r;
+      float wn = 0.f;
+      if (li < k) {
+        double d = den[r];
+        const double wold = (double)wso[s * k + li];
+        if (l1 > 0.0) d += l1;              // SK:616-617
+        if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
+        if (d == 0.0) d = EPS32;            // SK:620
+        wn = (float)(wold * (num64[r] / d));  // SK:622-629
+      }
+      wr[r] = wn;
+      float* dst = li < k ? W + (size_t)(r0 + s) * k + li : dummy + 256 * r;
+      *dst = wn;
+    }
+    STAMP(4);  // 4: phase 2 (+ the W' stores)
+    if (!do_acc) return;
+    // phase 3: A[m = 4g + r][f = 16nb + li] and B[m][n] over the tile's 16 samples
+    s16x4 a1, a2, a3;  // w'[4g + j][li] in three bf16 terms: the A operand (row m = li, k = 4g + j)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint16_t h1 = bm::bf16_rn(wr[j]);
+      const float r1 = wr[j] - bm::bf16_f(h1);
+      const uint16_t h2 = bm::bf16_rn(r1);
+      const float r2 = r1 - bm::bf16_f(h2);
+      a1[j] = (short)h1;
+      a2[j] = (short)h2;
+      a3[j] = (short)bm::bf16_rn(r2);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
+    const int q = li >> 2, p = li & 3;
+    const unsigned char* xb0 = xs + ((size_t)(4 * g + q) * F + 4 * p) * 2;
+#pragma unroll
+    for (int nb = 0; nb < NBX; ++nb) {
+      if (nb < (KSC ? 2 * KSC : NB)) {
+        const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb0 + 32 * nb));
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a3, b, cacc[nb], 0, 0, 0);
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, b, cacc[nb], 0, 0, 0);
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, b, cacc[nb], 0, 0, 0);
+      }
+    }
+    STAMP(5);  // 5: phase 3
+  };
+
+  u32x4 pf[PD][PFS];
+#pragma unroll
+  for (int s0 = 0; s0 < PD; ++s0) {
+    prefetch(pf[s0], s0);
+#pragma unroll
+    for (int d = 0; d < NSTB; ++d) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy + 256 * d), "v"(0) : "memory");
+  }
+  int nx = PD;
+  for (int i0 = 0; i0 < ntw; i0 += PD) {
+#pragma unroll
+    for (int s0 = 0; s0 < PD; ++s0) {
+      STAMP(0);
+      // younger than this set: the PD - 1 later sets and the stores of the PD bodies since
+      wait_set<PFS * (PD - 1) + NSTB * PD>(pf[s0]);
+      STAMP(1);  // 1: wait for the set
+      stage(pf[s0]);
+      prefetch(pf[s0], nx);
+      ++nx;
+      STAMP(2);  // 2: stage + prefetch issue
+      if (i0 + s0 < ntw) body(i0 + s0);
+      STAMP(6);  // 6: the fold (every QF tiles) and the loop
+    }
+  }
+  STAMP_FLUSH;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
+  if (!do_acc) return;
+
+  // ---- the workgroup's partial row [k][F + k]: the waves' sums in the order (w0 + w2) + (w1 + w3)
+  __syncthreads();  // every wave done with its slot: LDS is reused from offset 0
+  double* red = reinterpret_cast<double*>(smem);  // [2][NBX + 1][4][64]
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int nb = 0; nb < NBX; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[((slot * (NBX + 1) + nb) * 4 + r) * 64 + l] = (double)cacc[nb][r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[((slot * (NBX + 1) + NBX) * 4 + r) * 64 + l] = (double)bacc[r];
+  };
+  double sa64[NBX + 1][4];
+#pragma unroll
+  for (int nb = 0; nb < NBX; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sa64[nb][r] = (double)cacc[nb][r];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sa64[NBX][r] = (double)bacc[r];
+  if (w >= 2) put(w - 2);
+  __syncthreads();
+  if (w < 2)
+#pragma unroll
+    for (int nb = 0; nb <= NBX; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sa64[nb][r] += red[((w * (NBX + 1) + nb) * 4 + r) * 64 + l];
+  __syncthreads();
+  if (w == 1)
+#pragma unroll
+    for (int nb = 0; nb <= NBX; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[(nb * 4 + r) * 64 + l] = sa64[nb][r];
+  __syncthreads();
+  if (w != 0) return;
+  const int V = F + k;
+  double* prow = partials + (size_t)blockIdx.x * k * V;
+#pragma unroll
+  for (int nb = 0; nb <= NBX; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double v = sa64[nb][r] + red[(nb * 4 + r) * 64 + l];
+      const int m = 4 * g + r;
+      if (nb < NBX) {
+        const int f = 16 * nb + li;
+        if (m < k && f < F) prow[(size_t)m * V + f] = v;
+      } else if (m < k && li < k) {
+        prow[(size_t)m * V + F + li] = v;
+      }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // The sample-lane pass: the IOP grid's headline shape (F = 81, k = 4, fp32 X and W), full tiles.
 //
 // mu_pass_kernel spends most of its issue slots and LDS cycles on moving data between lane
@@ -2109,11 +2421,6 @@ __device__ unsigned long long g_tl_pub[TL_IT];
 __device__ unsigned long long g_tl_x[TL_IT * 4];  // MULTI exchange: start, stored, flags seen, summed
 __device__ unsigned long long g_tl_start[TL_WG];
 __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits), HW_REG_XCC_ID
-__device__ unsigned long long g_tl_rs[TL_IT * TL_WG * 3];  // layout 6: rows seen, columns published, AB seen
-#define TL_RS(it_, slot_)                                                                        \
-  do {                                                                                          \
-    if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_rs[((it_) * TL_WG + b) * 3 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
 #define TL(it_, slot_)                                                                          \
   do {                                                                                          \
     if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
@@ -2133,7 +2440,6 @@ __device__ unsigned long long g_tl_rs[TL_IT * TL_WG * 3];  // layout 6: rows see
   } while (0)
 #else
 #define TL(it_, slot_) do {} while (0)
-#define TL_RS(it_, slot_) do {} while (0)
 #define TL_PUB(it_) do {} while (0)
 #define TL_X(it_, slot_) do {} while (0)
 #define TL_START do {} while (0)
@@ -2660,10 +2966,7 @@ struct Geo {
   static constexpr int L_HHT = L_HT + NL * NQ * KK * 4;                 // HHᵀ fp64 [K][K]
   static constexpr int L_FLAG = L_HHT + KK * KK * 8;                    // 8 ints
   static constexpr int L_LOSS = L_FLAG + 32;                            // [NWV] wave loss sums, init, prev
-  // RS: one fp64 value per (column, row) pair of the workgroup's columns (≤ NOUT + 1 + NT - 1)
-  static constexpr int RSV = NOUT + 1 + 256;
-  static constexpr int L_RSV = (L_LOSS + 8 * 8 + 15) / 16 * 16;
-  static constexpr int L_WRES = L_RSV + RSV * 8;                        // [NWV][nbt_max][WBW]
+  static constexpr int L_WRES = (L_LOSS + 8 * 8 + 15) / 16 * 16;        // [NWV][nbt_max][WBW]
   static_assert(NCHW * 16 == XBW && XBW % 16 == 0, "tiles are whole 16-byte chunks");
   static_assert(OVR >= 0 && PADB / 4 <= 64, "one zero float per lane covers the overrun");
   static_assert(NOUT <= 3 * NT, "three accumulator outputs per thread at most");
@@ -2933,26 +3236,7 @@ __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, doub
 // workgroup leaves with the state after g iterations: H (not updated), W as it was before this
 // iteration's update — written to W itself in the loss iterations when W is resident in LDS, else to
 // the snapshot buffer (TC_WSNAP; the host copies it) — so n_iter = g as in sklearn.
-//
-// RS (layout 6): the end of an iteration as ONE reduce-scatter over data-tagged granules instead of
-// the ticket tree (group combiners, top combiner, flag; 4.5 µs tail + 3.7 µs resume at cfg2,
-// DESIGN §3.0).  Every workgroup (1) publishes its fp64 row column-major, each value as two 8-byte
-// {tag = it + 1 : 32-bit half} granules (agent-scope stores: MI355X_MICROARCH.md R2 granules, the data
-// is the flag); (2) reduces its own columns c = b + G·j over the G rows in a fixed order (a poll of
-// its granules until every tag matches; rows in LDS; per column one wave's sequential + xor-tree
-// sum), (MULTI: exchanges those column sums with every rank, summed in rank order), and publishes the
-// sums as granules of AB; (3) polls all of AB, then applies the basis update itself.  Two hand-offs
-// per iteration, no counter, no flag.  A buffer is rewritten only after every reader of its previous
-// contents is done (a workgroup publishes row it + 1 after it has read all of AB(it), which needs
-// every column reduced, which needs every row read), so one buffer each suffices; the host zeroes
-// both before the launch (tags count within it).  The column sums' order is fixed (deterministic,
-// split launches bit-identical) but differs from the tree's, so layouts 4 and 6 agree to rounding.
-//
-// TAB (layout 7): the ticket tree of layout 4, but the top combiner publishes AB as data-tagged
-// granules (two per fp64 value, tag = it + 1) that every other workgroup polls directly: no flag,
-// and no separate AB load after it (one hand-off less in the resume); each workgroup takes the
-// tolerance decision itself from the same AB bits.
-template <int KK, bool WRES, int PD, bool MULTI = false, bool TOL = false, bool RS = false, bool TAB = false>
+template <int KK, bool WRES, int PD, bool MULTI = false, bool TOL = false>
 __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   using namespace wt;
   using G_ = Geo<KK>;
@@ -3082,15 +3366,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // rewritten at the iteration's end), so that every set — the first PD too — has exactly PD stores
   // younger than it when its step waits (set q < PD: PD - q dummies, then the W stores of bodies
   // 0..q-1).  Counting PD stores that were never issued would let the set's last loads (the W tile)
-  // still be in flight when it is staged.  (RS: into the stage buffer past AB's granules, a region
-  // nothing reads: the partial rows are handed off word by word, so a late dummy store must never be
-  // able to land on a published granule.)
-  // TAB: AB's granules in the stage buffer past the group rows (NG <= 16 for a grid of <= 256)
-  uint64_t* tabg = reinterpret_cast<uint64_t*>(a.groups + 32 * NOUTT);
-  float* dummy = RS ? reinterpret_cast<float*>(a.groups + 2 * NOUTT) + 64 * (gw & 63) + l
-                    : reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
-  if (RS && MULTI && t == 0)  // the launch's generation base (workgroup 0 advances it at its end)
-    sFlag[6] = (int)(uint32_t)__hip_atomic_load(a.xctl + XC_GEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // still be in flight when it is staged.
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
@@ -3116,258 +3393,6 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     stage(pfk);
     prefetch(pfk, gw + (int64_t)NW * nx_i);
     if (++nx_i == nbt) nx_i = 0;
-  };
-  // RS: the end of iteration `it` once the waves' sums are in `red` (the comment above the kernel).
-  // Returns true with the next iteration's basis in LDS, false when this workgroup leaves the launch
-  // (its last iteration, a tolerance stop, or a failed wait: then the error word is set).
-  // AB from its granules (two per fp64 value {tag : half}) into sAB, every value polled until both
-  // its granules carry the tag; returns 1 when the wait failed (timeout: the error word set here)
-  auto poll_ab = [&](const uint64_t* abg, uint32_t tag) -> int {
-    constexpr int UA = (NOUTT + NT - 1) / NT;  // AB values per thread
-    bool need[UA];
-#pragma unroll
-    for (int u = 0; u < UA; ++u) need[u] = t + NT * u < NOUTT;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // same batch
-      bool ok = true;
-#pragma unroll
-      for (int u = 0; u < UA; ++u)
-        if (need[u]) {
-          const int o = t + NT * u;
-          const uint64_t lo = __hip_atomic_load(abg + 2 * o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint64_t hi = __hip_atomic_load(abg + 2 * o + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag) {
-            sAB[o] = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
-            need[u] = false;
-          } else {
-            ok = false;
-          }
-        }
-      if (__all(ok)) return 0;
-      if (__builtin_amdgcn_readfirstlane(ev) != 0u) return 1;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 1;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-  };
-  auto put_granules = [&](uint64_t* p, double v, uint32_t tag) {  // one fp64 value as {tag : half} x 2
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    __hip_atomic_store(p, ((uint64_t)tag << 32) | (u & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(p + 1, ((uint64_t)tag << 32) | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto rs_end = [&](int it, bool last_it, bool loss_it) -> bool {
-    constexpr int UR = (G_::RSV + NT - 1) / NT;  // (column, row) pairs per thread, at most
-    uint64_t* pg = reinterpret_cast<uint64_t*>(a.partials);  // [G][NOUTT][2] granules
-    uint64_t* abg = reinterpret_cast<uint64_t*>(a.groups);   // [NOUTT][2] granules
-    double* rsv = reinterpret_cast<double*>(smem + G_::L_RSV);
-    const uint32_t tag = (uint32_t)(it + 1);
-    auto put = [&](uint64_t* p, double v) { put_granules(p, v, tag); };
-    // (1) this workgroup's row: value o as granules pg[(b·NOUTT + o)·2 + {0, 1}] (coalesced stores)
-    for (int o = t; o < NOUTT; o += NT) {
-      double val;
-      if (TOL && o == NOUT) {
-        val = (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]);
-      } else {
-        const int j = o / V;
-        const int v = o - j * V;
-        const int ee = v < F ? v / NQ : j;
-        const int idx = v < F ? (v - NQ * ee) * KK + j : NQ * KK + (v - F);
-        const float* rr = red + ee * NACC + idx;
-        constexpr int WS = NL * NACC;  // wave stride
-        val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
-      }
-      put(pg + ((size_t)b * NOUTT + o) * 2, val);
-    }
-    TL(it, 0);
-    // (2) this workgroup's columns c = b + G·j over the G rows: every (column, row) pair polled
-    // until both its granules carry the tag, the values to LDS
-    const int ncol = b < NOUTT ? (NOUTT - 1 - b) / G + 1 : 0;
-    const int npair = ncol * G;
-    int fail = 0;
-    {
-      size_t off[UR];
-      bool need[UR];
-#pragma unroll
-      for (int u = 0; u < UR; ++u) {
-        const int q = t + NT * u;
-        need[u] = q < npair;
-        const int j = q / G, r = q - (q / G) * G;
-        off[u] = ((size_t)r * NOUTT + (b + G * j)) * 2;
-      }
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (true) {
-        // the error word in the same batch as the granules (one round trip per round)
-        const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ok = true;
-#pragma unroll
-        for (int u = 0; u < UR; ++u)
-          if (need[u]) {
-            const uint64_t lo = __hip_atomic_load(pg + off[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t hi = __hip_atomic_load(pg + off[u] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(lo >> 32) == tag && (uint32_t)(hi >> 32) == tag) {
-              rsv[t + NT * u] = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
-              need[u] = false;
-            } else {
-              ok = false;
-            }
-          }
-        if (__all(ok)) break;
-        if (__builtin_amdgcn_readfirstlane(ev) != 0u) {
-          fail = 1;
-          break;
-        }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
-          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          fail = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    if (__syncthreads_or(fail)) return false;
-    TL_RS(it, 0);
-    // (3) per column one wave: its lanes' rows in sequence, a fixed xor tree, lane 0's value (the
-    // same bits on every rank and run); MULTI: the ranks' sums for the column in rank order
-    for (int j = w; j < ncol; j += NWV) {
-      double sum = 0.0;
-      for (int r = l; r < G; r += 64) sum += rsv[j * G + r];
-      sum = __shfl(wave_sum(sum), 0, 64);
-      const int c = b + G * j;
-      if constexpr (MULTI) {
-        const int xrank = (int)__hip_atomic_load(a.xctl + XC_RANK, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int xworld = (int)__hip_atomic_load(a.xctl + XC_WORLD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t gen = (uint32_t)sFlag[6] + (uint32_t)it + 1u;
-        const size_t slot = 2 * (size_t)NOUTT;
-        const size_t par = (size_t)(gen & 1u) * xworld * slot;
-        const bool bad = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-        const uint64_t xt = (uint64_t)(bad ? sl::XPOISON : gen) << 32;
-        const uint64_t u = (uint64_t)__double_as_longlong(sum);
-        if (l < xworld) {  // lane p -> rank p's buffer, slot xrank
-          uint64_t* peer = reinterpret_cast<uint64_t*>(
-              __hip_atomic_load(a.xctl + XC_PEERS + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          uint64_t* dst = peer + par + (size_t)xrank * slot + 2 * c;
-          __hip_atomic_store(dst, xt | (u & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(dst + 1, xt | (u >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-        const uint64_t* mine = reinterpret_cast<const uint64_t*>(
-            __hip_atomic_load(a.xctl + XC_PEERS + xrank, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        const uint64_t* src = mine + par + (size_t)min(l, xworld - 1) * slot + 2 * c;  // lane q: rank q's
-        uint64_t lo = 0, hi = 0;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (true) {
-          const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          lo = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          hi = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          const uint32_t tl = (uint32_t)(lo >> 32), th = (uint32_t)(hi >> 32);
-          if (__all(tl == gen && th == gen)) break;
-          if (__any(tl == sl::XPOISON || th == sl::XPOISON)) {
-            __hip_atomic_store(err, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            fail = 1;
-            break;
-          }
-          if (__builtin_amdgcn_readfirstlane(ev) != 0u) {
-            fail = 1;
-            break;
-          }
-          if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
-            __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            fail = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (fail) break;
-        const double vq = __longlong_as_double((long long)((hi << 32) | (lo & 0xFFFFFFFFull)));
-        sum = 0.0;
-        for (int q = 0; q < xworld; ++q) sum += __shfl(vq, q, 64);  // rank order
-      }
-      if (l == 0) put(abg + 2 * c, sum);
-    }
-    if (__syncthreads_or(fail)) return false;
-    TL_RS(it, 1);
-    // (4) all of AB from its granules
-    fail = poll_ab(abg, tag);
-    if (__syncthreads_or(fail)) return false;
-    TL_RS(it, 2);
-    if (b == 0) TL_PUB(it);
-    // (5) the tolerance test (SK:872-884) on the state after it0 + it iterations: every workgroup
-    // decides from the same AB bits; workgroup 0 keeps the host's record
-    if (TOL && loss_it) {
-      if (t == 0) {
-        const int gi = it0 + it;
-        const double errv = sqrt(fmax(sAB[NOUT], 0.0));
-        int stop = 0;
-        if (b == 0) {
-          const int slot = gi / 10;
-          if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
-          st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
-        }
-        if (gi == 0) {
-          sLoss[4] = sLoss[5] = errv;
-          if (b == 0) {
-            st_sc1(a.tolctl + TC_INIT, errv);
-            st_sc1(a.tolctl + TC_PREV, errv);
-          }
-        } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
-          stop = 1;
-        } else {
-          sLoss[5] = errv;
-          if (b == 0) st_sc1(a.tolctl + TC_PREV, errv);
-        }
-        sFlag[3] = stop;
-      }
-      __syncthreads();
-      if (sFlag[3]) {  // stopped: the state after it0 + it iterations (W already in place, H = sH)
-        if (b != 0) return false;
-        for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
-        for (int o = t; o < F * KK; o += NT) {
-          const int f = o / KK;
-          const int j = o - f * KK;
-          a.Ht[o] = sH[j * F + f];
-        }
-        if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
-        if (t == 0) {
-          st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
-          st_sc1(a.tolctl + TC_STOPPED, 1.0);
-          st_sc1(a.tolctl + TC_IN_SNAP, WRES ? 0.0 : 1.0);
-          if (MULTI)
-            __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return false;
-      }
-    }
-    if (last_it) {
-      if (WRES)  // this wave's W back to HBM, once per launch
-        for (int c = l; c < nbt * (WBW / 16); c += 64) {
-          const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
-          *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
-              *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
-        }
-      if (b != 0) return false;
-      for (int o = t; o < NOUTT; o += NT) a.AB[o] = sAB[o];  // the last iteration's accumulators
-      if (a.apply_last) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
-      for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
-      for (int o = t; o < F * KK; o += NT) {
-        const int f = o / KK;
-        const int j = o - f * KK;
-        a.Ht[o] = sH[j * F + f];
-      }
-      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
-      if (t == 0) {
-        if (TOL) {
-          st_sc1(a.tolctl + TC_DONE, (double)(it0 + a.n_iter));
-          st_sc1(a.tolctl + TC_STOPPED, 0.0);
-        }
-        if (MULTI)  // the next launch's generations follow this one's
-          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return false;
-    }
-    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
-    return true;
   };
   auto body = [&]() {
     const int it = cur_it, i = cur_i;
@@ -3544,15 +3569,6 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       lossacc = 0.0;
     }
     __syncthreads();
-    if constexpr (RS) {
-      if (!rs_end(it, last_it, loss_it)) {
-        alive = false;
-        return;
-      }
-      load_basis();
-      TL(it, 1);
-      return;
-    }
     // the workgroup's fp64 row [K][V] (+ the loss): the four waves' sums in wave order (deterministic)
     {
       double* prow = a.partials + (size_t)b * NOUTT;
@@ -3596,8 +3612,6 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       if (sFlag[1]) {  // top combiner: AB
         sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
-        if (TAB && must_wait)  // AB as granules for the others (this thread's own outputs of the sums)
-          for (int o = t; o < NOUTT; o += NT) put_granules(tabg + 2 * o, sAB[o], (uint32_t)(it + 1));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         // (after the barrier: the summed loss sAB[NOUT] was written by another thread)
@@ -3619,33 +3633,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
           }
         }
         if (TOL && loss_it) __syncthreads();  // sFlag[3] (the decision) for the whole workgroup
-        if (!TAB && t == 0 && must_wait)
+        if (t == 0 && must_wait)
           __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         TL_PUB(it);
       }
     }
     const bool top = sFlag[1] != 0;
-    if (TAB && !top && must_wait) {  // AB straight from the top's granules
-      if (__syncthreads_or(poll_ab(tabg, (uint32_t)(it + 1)))) {
-        alive = false;
-        return;
-      }
-      if (TOL && loss_it) {  // the top's decision, taken here from the same AB bits and state
-        if (t == 0) {
-          const double errv = sqrt(fmax(sAB[NOUT], 0.0));
-          int stop = 0;
-          if (it0 + it == 0)
-            sLoss[4] = sLoss[5] = errv;
-          else if ((sLoss[5] - errv) / sLoss[4] < tolv)
-            stop = 1;
-          else
-            sLoss[5] = errv;
-          sFlag[3] = stop;
-        }
-        __syncthreads();
-      }
-    } else if (!top && must_wait) {
+    if (!top && must_wait) {
       if (t == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -3728,7 +3723,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       return;
     }
-    if (!TAB && !top) {
+    if (!top) {
       for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
       if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
@@ -5076,6 +5071,19 @@ static bool use_sl(int x_dtype, int F, int k) {
 static bool use_bf16_mfma(int x_dtype, int F, int k) {
   return x_dtype == CNMF_BF16 && k >= 9 && k <= 16 && F % 4 == 0 && F <= 64 * bm::NBW_MAX &&
          bm::lds(F).total <= (int)(160 * 1024);
+}
+
+// the wave-tile bf16 pass (mu_pass_bfw_kernel) serves the accumulating / updating passes of the
+// bf16 matrix-core shapes over their full 64-sample tiles (the ragged tail: one workgroup of
+// mu_pass_bf16_mfma_kernel); CNMF_BFW=0 (diagnostic build) keeps the 64-sample kernel for A/B runs
+static bool g_no_bfw = diag_env("CNMF_BFW") && atoi(diag_env("CNMF_BFW")) == 0;
+static bool use_bfw(int x_dtype, int F, int k) {
+  return !g_no_bfw && !g_force_valu && use_bf16_mfma(x_dtype, F, k) && F >= 8 && F <= 16 * bw::NBX &&
+         k * (F + k) >= 512 && bw::lds(F).total <= (int)kMaxLds;
+}
+static PassFn bfw_fn(int F, int k) {
+  return (bm::ksteps(F) == 10 && k == 16) ? reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<10, 16>)
+                                          : reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<0, 0>);
 }
 
 static int select_pass(int x_dtype, int F, int k, PassKernel* pk, size_t* lds, bool mfma_ok = true) {
@@ -6486,6 +6494,15 @@ static int64_t sl_grid(int64_t n_rows, int64_t* n_full, bool* tail) {
 }
 
 static int64_t main_grid(int64_t n_rows, int x_dtype, int F, int k, PassKernel* pk, size_t* lds) {
+  if (use_bfw(x_dtype, F, k)) {  // the wave-tile grid over the full tiles, + one row for a ragged tail
+    const int64_t n_full = n_rows / TS;
+    int64_t g = 0;
+    if (n_full > 0) {
+      g = pass_grid(n_full * TS, bfw_fn(F, k), (size_t)bw::lds(F).total);
+      if (g < 0) return -1;
+    }
+    return g + (n_rows % TS != 0 ? 1 : 0);
+  }
   if (use_sl(x_dtype, F, k)) {
     int64_t n_full;
     bool tail;
@@ -6554,6 +6571,28 @@ int cnmf_mu_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, c
     int64_t rows = n_rows - n_full * TS, one = 1;
     void* args[] = {(void*)&Xt, &Wt, (void*)&Ht, (void*)&HHt, &pt, &rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&one};
     HIP_CHECK(hipLaunchKernel(pk.fn, dim3(1), dim3(NT), args, lds, s));
+    return CNMF_OK;
+  }
+  if (use_bfw(x_dtype, n_features, k) && (flags & CNMF_PASS_UPDATE_W) && partials) {
+    const int64_t n_full = n_rows / TS;
+    int64_t g = 0;
+    if (n_full > 0) {
+      const size_t lb = (size_t)bw::lds(F).total;
+      g = pass_grid(n_full * TS, bfw_fn(F, k), lb);
+      if (g <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+      int64_t nt = n_full;
+      void* args[] = {(void*)&X, &W, (void*)&Ht, (void*)&HHt, &partials, &n_rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&nt};
+      HIP_CHECK(hipLaunchKernel(bfw_fn(F, k), dim3((unsigned)g), dim3(NT), args, lb, s));
+    }
+    if (n_rows % TS == 0) return CNMF_OK;
+    // the ragged tail (< 64 rows) on one workgroup of the 64-sample matrix-core pass, partial row g
+    if (max_resident(pmain.fn, lmain) <= 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
+    const void* Xt = static_cast<const bf16_t*>(X) + n_full * TS * F;
+    void* Wt = static_cast<float*>(W) + n_full * TS * k;
+    double* pt = partials ? partials + g * (int64_t)k * (F + k) : nullptr;
+    int64_t rows = n_rows - n_full * TS, one = 1;
+    void* args[] = {(void*)&Xt, &Wt, (void*)&Ht, (void*)&HHt, &pt, &rows, &F, &k, &l1_W, &l2_W, &flags, (void*)&one};
+    HIP_CHECK(hipLaunchKernel(pmain.fn, dim3(1), dim3(NT), args, lmain, s));
     return CNMF_OK;
   }
   PassKernel pk = pmain;
@@ -6786,10 +6825,6 @@ int cnmf_debug_hstep(unsigned long long* host_out) {  // [64 calls][4 rows][BPP 
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hs), sizeof(unsigned long long) * 64 * 4 * 2));
   return CNMF_OK;
 }
-int cnmf_debug_rs_timeline(unsigned long long* host_out) {  // [TL_IT][TL_WG][3]
-  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_rs), sizeof(unsigned long long) * TL_IT * TL_WG * 3));
-  return CNMF_OK;
-}
 int cnmf_debug_xtimeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
   return CNMF_OK;
@@ -6872,15 +6907,14 @@ static int default_layout() {
 }
 static int resolve_layout(int layout) {
   if (layout == 0) return default_layout();
-  return (layout >= 1 && layout <= 7) ? layout : -1;
+  return (layout >= 1 && layout <= 5) ? layout : -1;
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
       return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles), " \
-                     "4 (wave tiles), 5 (k = 8 wave tiles on the matrix cores), 6 (wave tiles, reduce-scatter "  \
-                     "end of iteration) or 7 (wave tiles, AB as tagged granules)");                       \
+                     "4 (wave tiles) or 5 (k = 8 wave tiles on the matrix cores)");                       \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
@@ -6946,17 +6980,7 @@ static int wt_pd(int k, bool wres, bool multi) {
 }
 extern "C++" {
 template <int KK, bool WRES>
-static PassFn wt_fn_k(int pd, bool multi, bool tol, bool rs, bool tab) {
-  if (tab)  // layout 7: the ticket tree with AB published as tagged granules, PD = 3
-    return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true, false, true>)
-                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true, false, true>))
-               : (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, false, false, true>)
-                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, false, false, true>));
-  if (rs)  // layout 6: the reduce-scatter end of iteration, PD = 3
-    return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true, true>)
-                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true, true>))
-               : (multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, false, true>)
-                        : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, false, true>));
+static PassFn wt_fn_k(int pd, bool multi, bool tol) {
   if (tol)  // the device tolerance test: PD = 3
     return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true>)
                  : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true>);
@@ -6977,10 +7001,10 @@ static PassFn mf8_fn(bool wres, bool multi, bool tol) {
              : (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, true, false>)
                       : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, false>));
 }
-static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false, bool rs = false, bool tab = false) {
-  const int pd = (tol || rs || tab) ? 3 : wt_pd(k, wres, multi);
-  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol, rs, tab) : wt_fn_k<4, false>(pd, multi, tol, rs, tab);
-  return wres ? wt_fn_k<8, true>(pd, multi, tol, rs, tab) : wt_fn_k<8, false>(pd, multi, tol, rs, tab);
+static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false) {
+  const int pd = tol ? 3 : wt_pd(k, wres, multi);
+  if (k == 4) return wres ? wt_fn_k<4, true>(pd, multi, tol) : wt_fn_k<4, false>(pd, multi, tol);
+  return wres ? wt_fn_k<8, true>(pd, multi, tol) : wt_fn_k<8, false>(pd, multi, tol);
 }
 static int device_cus() {
   static int cus[64] = {0};
@@ -6994,18 +7018,14 @@ struct WtLaunch {
   int64_t G, n_tiles;
   size_t lds;
   bool mf;  // k = 8 on the matrix cores (mu_iter_mf8_kernel)
-  bool rs;  // layout 6: the reduce-scatter end of iteration (partials hold 2·G rows of granules)
-  int k;
-  bool tab;  // layout 7: the ticket tree, AB published as tagged granules (stage rows 32..)
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
 static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, WtLaunch* out,
                     bool tol = false) {
   if (x_dtype != CNMF_F32 || F != wt::F || (k != 4 && k != 8) || n_rows <= 0) return false;
-  if (k == 4 && layout != 4 && layout != 6 && layout != 7) return false;
-  if (k == 8 && layout != 4 && layout != 5 && layout != 6 && layout != 7) return false;
-  const bool rs = layout == 6, tab = layout == 7;
+  if (k == 4 && layout != 4) return false;
+  if (k == 8 && layout != 4 && layout != 5) return false;
   // k = 8, layout 4: the VALU wave tiles (8-sample tiles); layout 5 (rows a multiple of 16): the
   // matrix-core wave tiles (16-sample tiles; slower than layout 4 on the MI355X measured)
   const bool mf = k == 8 && layout == 5 && n_rows % 16 == 0;
@@ -7016,7 +7036,7 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
   const int ncu = device_cus();
   const int64_t n_tiles = n_rows / tsw;
   for (int wres = 1; wres >= 0; --wres) {
-    const int pd = (tol || rs || tab) ? 3 : wt_pd(k, wres != 0, multi);
+    const int pd = tol ? 3 : wt_pd(k, wres != 0, multi);
     // tiles per wave: > PD (the first prefetches), >= 2·PD + 1 when W is streamed (re-load hazard)
     const int min_nbt = wres ? pd + 1 : 2 * pd + 1;
     const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
@@ -7024,9 +7044,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
     if (lds > kMaxLds) continue;
-    const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol, rs, tab);
+    const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
-    *out = WtLaunch{fn, G, n_tiles, lds, mf, rs, k, tab};
+    *out = WtLaunch{fn, G, n_tiles, lds, mf};
     return true;
   }
   return false;
@@ -7154,19 +7174,10 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
                         n_features, k, sum_to_one, smoothness, xctl, events, n_events, stream);
 }
 
-// the wave-tile launch of this shape and layout that the buffers can serve: layout 6 keeps its
-// granules in the partials (2·G rows of k(F+k)+1 doubles, column-major) — with fewer rows the
-// ticket tree of layout 4 serves the shape
-static bool wt_plan_n(int64_t n_rows, int x_dtype, int F, int k, bool multi, int layout, int64_t n_parts,
-                      WtLaunch* L, bool tol = false) {
-  if (wt_plan(n_rows, x_dtype, F, k, multi, layout, L, tol) && L->G <= n_parts && (!L->rs || 2 * L->G + 2 <= n_parts))
-    return true;
-  return layout == 6 && wt_plan(n_rows, x_dtype, F, k, multi, 4, L, tol) && L->G <= n_parts;
-}
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
                      double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
                      double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl,
-                     double* tolctl = nullptr, void* const* events = nullptr, int n_events = 0) {
+                     double* tolctl = nullptr) {
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
   PersistArgs pa;
@@ -7192,15 +7203,7 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.xctl = xctl;
   pa.tolctl = tolctl;
   void* args[] = {&pa};
-  const size_t noutt = (size_t)L.k * (wt::F + L.k) + (tolctl ? 1 : 0);
-  if (L.rs) {  // every granule's tag back to 0 (tags count iterations within the launch)
-    HIP_CHECK(hipMemsetAsync(partials, 0, 2 * (size_t)L.G * noutt * sizeof(double), s));
-    HIP_CHECK(hipMemsetAsync(stage, 0, 2 * noutt * sizeof(double), s));
-  }
-  if (L.tab) HIP_CHECK(hipMemsetAsync(stage + 32 * noutt, 0, 2 * noutt * sizeof(double), s));
-  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), s));
   HIP_CHECK(hipLaunchKernel(L.fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, s));
-  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), s));
   return CNMF_OK;
 }
 
@@ -7235,11 +7238,8 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
     else
       snprintf(out, (size_t)len,
                "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
-               "(%lld workgroups), no barrier inside an iteration; %s",
-               k, wres ? "resident in LDS" : "streamed with X", L.rs ? 3 : wt_pd(k, wres, false), 64 / k, (long long)L.G,
-               L.rs ? "end of iteration: one reduce-scatter over tagged granules (layout 6)"
-                    : (L.tab ? "end of iteration: ticket tree, AB as tagged granules (layout 7)"
-                             : "end of iteration: ticket tree + flag (layout 4)"));
+               "(%lld workgroups), no barrier inside an iteration",
+               k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
     return 1;
   }
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
@@ -7440,7 +7440,7 @@ int cnmf_mu_shard_step(const void* X, int x_dtype, void* W, double* H64, double*
   {  // one wave-tile launch with n_iter = 1: the multi-iteration launch's layout, so the RCCL path
      // and the in-launch exchange sum the same partials; only tickets, no waits
     WtLaunch L;
-    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, layout >= 6 ? 4 : layout, &L) && L.G <= n_parts)
+    if (partials && wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts)
       return launch_wt(L, 1, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
                        apply_first, 0, hs, nullptr);
   }
@@ -7508,11 +7508,15 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
   RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan_n(n_rows, x_dtype, n_features, k, false, layout, n_parts, &L)) {
+    if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L) && L.G <= n_parts) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
-      return launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H, 0, 1,
-                       hs, nullptr, nullptr, events, n_events);
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
+                               l2_H, 0, 1, hs, nullptr);
+      if (st) return st;
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+      return CNMF_OK;
     }
   }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
@@ -7576,11 +7580,15 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
   RESOLVE_LAYOUT(layout);
   {
     WtLaunch L;
-    if (wt_plan_n(n_rows, x_dtype, n_features, k, true, layout, n_parts, &L)) {
+    if (wt_plan(n_rows, x_dtype, n_features, k, true, layout, &L) && L.G <= n_parts) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !xctl)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
-      return launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H, 0, 1,
-                       hs, xctl, nullptr, events, n_events);
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+      const int st = launch_wt(L, n_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H,
+                               l2_H, 0, 1, hs, xctl);
+      if (st) return st;
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+      return CNMF_OK;
     }
   }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k, true);
@@ -7610,17 +7618,18 @@ int cnmf_mu_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H
   RESOLVE_LAYOUT(layout);
   if (max_iter <= 0) return set_err(CNMF_ERR_ARG, "max_iter must be >= 1");
   WtLaunch L;
-  if (!wt_plan_n(n_rows, x_dtype, n_features, k, xctl != nullptr, layout, n_parts < 0 ? 0 : n_parts, &L, true) &&
-      !wt_plan(n_rows, x_dtype, n_features, k, xctl != nullptr, layout == 6 ? 4 : layout, &L, true))
+  if (!wt_plan(n_rows, x_dtype, n_features, k, xctl != nullptr, layout, &L, true))
     return set_err(CNMF_ERR_UNSUPPORTED, "the device tolerance test serves the wave-tile launch (fp32 X, F = 81, "
-                   "k = 4 or 8, layout 4 or 6; n_rows=%lld F=%d k=%d layout=%d)", (long long)n_rows, n_features, k, layout);
+                   "k = 4 or 8, layout 4; n_rows=%lld F=%d k=%d layout=%d)", (long long)n_rows, n_features, k, layout);
   if (L.G > n_parts) return set_err(CNMF_ERR_ARG, "partials hold %lld rows, the persistent grid needs %lld",
                                     (long long)n_parts, (long long)L.G);
   if (!X || !W || !H64 || !Ht || !HHt || !partials || !stage || !counter || !AB || !tolctl)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   const int st = launch_wt(L, max_iter, X, W, H64, Ht, HHt, partials, stage, counter, AB, l1_W, l2_W, l1_H, l2_H,
-                           0, 1, hs, xctl, tolctl, events, n_events);
+                           0, 1, hs, xctl, tolctl);
   if (st) return st;
+  if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   // the iteration flag may still hold the last (or the stopping) iteration: cleared in stream order
   HIP_CHECK(hipMemsetAsync(counter + CNT_FLAG, 0, sizeof(uint32_t), hs));
   return CNMF_OK;

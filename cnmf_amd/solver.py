@@ -434,11 +434,9 @@ class MUPlan:
             self._allreduce(self.AB)
         self.basis_update()
 
-    def tune(self, n_iter: int = 100, rounds: int = 2, variants=(4, 7, 6, 1, 2)) -> dict:
+    def tune(self, n_iter: int = 100, rounds: int = 2, variants=(4, 1, 2)) -> dict:
         """Time the layouts of the persistent launch (the `layout` argument, include/cnmf_hip.h:
-        4 = wave tiles, 7 = wave tiles with AB as tagged granules, 6 = wave tiles with the
-        reduce-scatter end of iteration, 1 = pairs of 4-wave
-        workgroups, 2 = 8-wave two-team workgroups; 3 = pairs
+        4 = wave tiles, 1 = pairs of 4-wave workgroups, 2 = 8-wave two-team workgroups; 3 = pairs
         with floating tiles is not bit-repeatable and only timed when asked for) on this plan's
         shape and keep the fastest for THIS plan.  Runs on copies of W and H: the plan's state is
         unchanged.  Collective over the plan's group: every rank times the same launches in the
@@ -449,8 +447,8 @@ class MUPlan:
         (empty dict) for non-persistent plans."""
         if not self.persistent or self.k not in (4, 8) or self.xdt != _lib.F32:
             return {}  # the layouts are alternatives for fp32 k = 4 and k = 8 only
-        if self.k == 8:  # k = 8: the VALU wave tiles (4, 6) or the matrix-core wave tiles (5)
-            variants = (4, 7, 6, 5)
+        if self.k == 8:  # k = 8: the VALU wave tiles (4) or the matrix-core wave tiles (5)
+            variants = (4, 5)
         W0, H0 = self.W.clone(), self.H64.clone()
         keep = self.layout
         times = {v: [] for v in variants}

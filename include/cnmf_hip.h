@@ -117,13 +117,7 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *       rest is drawn from a pool every iteration (not bit-repeatable: the draw decides the order).
  *   5 = k = 8 only: the wave tiles with both products on the matrix cores (v_mfma_f32_16x16x4_f32,
  *       16-sample tiles; n_rows a multiple of 16, else layout 4);
- *   6 = layout 4 with the end of an iteration as one reduce-scatter over data-tagged granules (every
- *       workgroup reduces its own columns of [WᵀX | WᵀW] over all partial rows, then reads all of
- *       AB): no ticket tree, no flag.  Needs n_parts >= 2·G + 2 (else layout 4 runs); the shard step
- *       (cnmf_mu_shard_step) runs layout 4 for it;
- *   7 = layout 4 with AB published by the top combiner as data-tagged granules that the other
- *       workgroups poll directly (no flag, no AB load after it); the shard step runs layout 4;
- * MUPlan.tune() times 4, 7, 6, 1 and 2 (k = 4) or 4, 7, 6 and 5 (k = 8) and keeps the fastest for its plan;
+ * MUPlan.tune() times 4, 1 and 2 (k = 4) or 4 and 5 (k = 8) and keeps the fastest for its plan;
  * other values are CNMF_ERR_ARG. */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0

@@ -72,25 +72,23 @@ def test_cfg3_sharded_k8_matches_oracle(tol, n_iter, N):
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
 
 
-def _plan(X, W0, H0, layout=0):
+def _plan(X, W0, H0):
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1])
-    plan.layout = layout
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("layout", [4, 6, 7])
-def test_cfg3_full_shard_k8(layout):
+def test_cfg3_full_shard_k8():
     import torch
     from cnmf_amd.synthetic import iop_spectra, random_init
     N = 1_250_000  # one GPU's share of cfg3's 1e7 rows over 8 GPUs
     X = iop_spectra(N, 81, seed=3, dtype=np.float32)
     W0, H0 = random_init(X, 8, 42)
-    a, b = _plan(X, W0, H0, layout), _plan(X, W0, H0, layout)
+    a, b = _plan(X, W0, H0), _plan(X, W0, H0)
     assert a.persistent  # the k = 8 wave-tile kernel, W streamed (40 MB of W: no LDS residency)
     a.iterate(20)
     b.iterate(7)
@@ -111,14 +109,13 @@ def test_cfg3_full_shard_k8(layout):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("layout", [4, 6, 7])
-def test_cfg2_full_size_500_iterations(layout):
+def test_cfg2_full_size_500_iterations():
     import torch
     from cnmf_amd.synthetic import iop_spectra, random_init
     N = 1_000_000
     X = iop_spectra(N, 81, seed=0, dtype=np.float32)
     W0, H0 = random_init(X, 4, 42)
-    plan = _plan(X, W0, H0, layout)
+    plan = _plan(X, W0, H0)
     assert plan.persistent
     plan.iterate(500)
     plan.check_sync_error()
@@ -132,8 +129,7 @@ def test_cfg2_full_size_500_iterations(layout):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("layout", [4, 6, 7])
-def test_wave_tiles_streamed_w_k4(layout):
+def test_wave_tiles_streamed_w_k4():
     """k = 4 past the LDS-resident W limit (2e6 rows: 31 KB of W per wave would not fit): the
     wave-tile kernel streams W with X; 30 iterations against the fp64 oracle, repeatable."""
     import torch
@@ -141,7 +137,7 @@ def test_wave_tiles_streamed_w_k4(layout):
     N = 2_000_000
     X = iop_spectra(N, 81, seed=12, dtype=np.float32)
     W0, H0 = random_init(X, 4, 42)
-    a, b = _plan(X, W0, H0, layout), _plan(X, W0, H0, layout)
+    a, b = _plan(X, W0, H0), _plan(X, W0, H0)
     assert a.persistent
     a.iterate(30)
     b.iterate(12)

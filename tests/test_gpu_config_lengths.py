@@ -37,6 +37,32 @@ def test_cfg4_500_iterations_matches_oracle():
 
 
 @pytest.mark.timeout(600)
+def test_cfg4_full_size_matches_oracle():
+    """cfg4 at its full 1e6 x 300 (k = 16): the wave-tile pass's fp32 MFMA accumulators chain over
+    every tile of a wave (≈ 61 per iteration), so the 1e6-row shape is checked against the fp64
+    oracle on the bf16-rounded X too (20 iterations: the oracle's cost), bar 1e-5."""
+    import torch
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X32 = iop_spectra(1_000_000, 300, seed=4, dtype=np.float32)
+    Xb = torch.from_numpy(X32).to(torch.bfloat16)
+    del X32
+    Xr = Xb.float().numpy()
+    W0, H0 = random_init(Xr, 16, 42)
+    plan = MUPlan(Xb.cuda(), 16)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.iterate(20)
+    torch.cuda.synchronize()
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = mu_ref.mu_fit(Xr.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=20, tol=0.0)
+    ew, eh = rel_fro(W, Wr), rel_fro(H, Hr)
+    print(f"cfg4 1e6 x 300 k16 bf16, 20 it: rel W {ew:.2e} rel H {eh:.2e}")
+    assert ew <= 1e-5 and eh <= 1e-5, (ew, eh)
+
+
+@pytest.mark.timeout(600)
 def test_cfg4_full_size_properties():
     import torch
     from cnmf_amd.solver import MUPlan

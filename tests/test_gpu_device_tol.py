@@ -17,11 +17,10 @@ from oracle import mu_ref
 pytestmark = pytest.mark.gpu
 
 
-def _plan(X, W0, H0, layout=0):
+def _plan(X, W0, H0):
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(torch.from_numpy(X).cuda(), W0.shape[1])
-    plan.layout = layout
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
@@ -32,12 +31,11 @@ def _plan(X, W0, H0, layout=0):
 @pytest.mark.parametrize("n,k,tol,max_iter", [(64 * 500, 4, 1e-4, 400), (64 * 500, 4, 1e-3, 500),
                                              (1_200_000, 8, 1e-3, 100), (64 * 3000, 4, 1e-6, 100),
                                              (64 * 3000, 4, 1e-6, 101)])
-@pytest.mark.parametrize("layout", [4, 6, 7])
-def test_device_tol_matches_oracle(n, k, tol, max_iter, layout):
+def test_device_tol_matches_oracle(n, k, tol, max_iter):
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(n, 81, seed=n % 97, dtype=np.float32)
     W0, H0 = random_init(X, k, 7)
-    plan = _plan(X, W0, H0, layout)
+    plan = _plan(X, W0, H0)
     res = plan.fit_device_tol(max_iter, tol)
     assert res is not None, "a wave-tile shape takes the device tolerance test"
     n_iter, errs = res

@@ -47,7 +47,7 @@ def _plan(X, W0, H0, group=None, layout=0):
     return plan
 
 
-@pytest.fixture(params=[4, 6, 7, 1, 2, 3], ids=["wave", "wave-rs", "wave-tab", "pairs", "teams", "floating"])
+@pytest.fixture(params=[4, 1, 2, 3], ids=["wave", "pairs", "teams", "floating"])
 def layout(request):
     """Every persistent layout a rank may pick (MUPlan.tune runs them all at N > 1 too); the
     multi-GPU launch serves layout 3 with layout 1 (floating tiles are single-GPU only)."""
@@ -83,7 +83,7 @@ def test_self_exchange_is_bit_identical(layout):
         dist.destroy_process_group()
 
 
-def _rank_main(rank, world, port, N, q, k=4, layout=0):
+def _rank_main(rank, world, port, N, q, k=4):
     try:
         import torch
         import torch.distributed as dist
@@ -92,7 +92,7 @@ def _rank_main(rank, world, port, N, q, k=4, layout=0):
                                 world_size=world)
         X, W0, H0 = _data(N, 7, k=k)
         lo, hi = rank * N // world, (rank + 1) * N // world
-        plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0, group=dist.group.WORLD, layout=layout)
+        plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0, group=dist.group.WORLD)
         plan.enable_exchange()
         plan.iterate(12)
         plan.iterate(18)
@@ -107,8 +107,8 @@ def _rank_main(rank, world, port, N, q, k=4, layout=0):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("k,layout", [(4, 4), (8, 4), (4, 6), (8, 6), (4, 7), (8, 7)])
-def test_two_ranks_one_gpu_exchange(k, layout):
+@pytest.mark.parametrize("k", [4, 8])
+def test_two_ranks_one_gpu_exchange(k):
     """Two processes on one GPU exchanging through IPC-mapped buffers inside the persistent launch
     (k = 8: cfg3's shape, the wave-tile kernel's xchg_allreduce_n over 712 accumulators)."""
     import torch
@@ -117,7 +117,7 @@ def test_two_ranks_one_gpu_exchange(k, layout):
     q = ctx.Queue()
     port = _port()
     env_keep = os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY")
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, N, q, k, layout)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, N, q, k)) for r in range(world)]
     for p in procs:
         p.start()
     out = {}
@@ -137,7 +137,7 @@ def test_two_ranks_one_gpu_exchange(k, layout):
     np.testing.assert_array_equal(H0_, H1_)  # rank-ordered sums: the same H everywhere
     W = np.concatenate([out[0][0], out[1][0]])
     X, W0, H0 = _data(N, 7, k=k)
-    ref = _plan(X, W0, H0, layout=layout)
+    ref = _plan(X, W0, H0)
     ref.iterate(30)
     ref.check_sync_error()
     torch.cuda.synchronize()
@@ -152,21 +152,20 @@ def test_two_ranks_one_gpu_exchange(k, layout):
     assert abs(out[0][2] - out[1][2]) <= 1e-12 * out[0][2]  # the loss all-reduce agrees too
 
 
-@pytest.mark.parametrize("N,layout", [(64 * 1500, 4), (1_250_048, 4), (64 * 1500, 6), (1_250_048, 6),
-                                      (64 * 1500, 7), (1_250_048, 7)])
-def test_self_exchange_k8(N, layout):
+@pytest.mark.parametrize("N", [64 * 1500, 1_250_048])
+def test_self_exchange_k8(N):
     """k = 8 (cfg3's shape) through the in-launch exchange with itself: the wave-tile kernel with W
     LDS-resident (96k rows) and streamed (a cfg3 shard), bit-identical to the single-GPU launch."""
     import torch
     import torch.distributed as dist
     X, W0, H0 = _data(N, 9, k=8)
-    ref = _plan(X, W0, H0, layout=layout)
+    ref = _plan(X, W0, H0)
     assert ref.persistent
     ref.iterate(14)
     ref.check_sync_error()
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1)
     try:
-        plan = _plan(X, W0, H0, group=dist.group.WORLD, layout=layout)
+        plan = _plan(X, W0, H0, group=dist.group.WORLD)
         plan.enable_exchange()
         assert plan.exchange and plan.persistent
         plan.iterate(5)

@@ -220,11 +220,14 @@ def test_factorise_normalise_option():
     np.testing.assert_allclose(np.linalg.norm(H.astype(np.float64), axis=1), 1.0, rtol=1e-6)
 
 
-@pytest.mark.parametrize("N, F, k", [(4096 + 29, 300, 16), (1000, 64, 12), (777, 300, 9), (3000, 124, 16)])
+@pytest.mark.parametrize("N, F, k", [(4096 + 29, 300, 16), (1000, 64, 12), (777, 300, 9), (3000, 124, 16),
+                                     (64 * 700, 300, 16), (40, 300, 16), (64 * 1000 + 16, 320, 13)])
 def test_bf16_mfma_single_pass_matches_numpy(N, F, k):
-    """§8 a8: the bf16 matrix-core pass (v_mfma_f32_16x16x32_bf16 with 3-term bf16 splits of H and
-    W', ds_read_b64_tr_b16 column reads): one W update and [WᵀX | WᵀW] vs NumPy fp64 on the
-    bf16-rounded X (ragged last tile, k < 16 padding)."""
+    """§8 a8: the bf16 matrix-core pass (the wave-tile mu_pass_bfw_kernel over the full 64-sample
+    tiles, the 64-sample mu_pass_bf16_mfma_kernel on a ragged tail: v_mfma_f32_16x16x32 /
+    16x16x16 bf16 with 3-term bf16 splits of H and W', ds_read_b64_tr_b16 column reads): one W
+    update and [WᵀX | WᵀW] vs NumPy fp64 on the bf16-rounded X (ragged last tile, no full tile at
+    all, whole tiles only, k < 16 padding, F = 320)."""
     import torch
     from cnmf_amd.solver import MUPlan
     from cnmf_amd import _lib

@@ -1,0 +1,13 @@
+#!/bin/bash
+# cfg4 wave-tile bf16 pass: its parity tests, the cfg4 bench line and the kernel-trace stats.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+D=gpurun_out/${1:-bfw}
+mkdir -p $D
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+T="python -u -m pytest -x -v -p no:cacheprovider --timeout 600 --timeout-method thread"
+timeout -k 10 600 $T -m gpu tests/test_gpu_parity.py -k "bf16" > $D/pytest_bf16.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --features 300 --k 16 --dtype bf16 --steps 100 --warmup 5 --no-cpu > $D/bench_cfg4.json 2> $D/bench_cfg4.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o cfg4 --output-format csv -- python3 bench.py --features 300 --k 16 --dtype bf16 --steps 50 --warmup 5 --no-cpu > $D/prof.log 2>&1 || exit 1
+timeout -k 10 900 $T -m gpu tests/test_gpu_config_lengths.py -k cfg4 > $D/pytest_cfg4.log 2>&1 || exit 1
+echo "exit=0"

@@ -13,6 +13,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 NAMES = ["", "stage wait+LDS write", "staging barrier", "prefetch issue", "phase 1", "phase 2 + barrier",
          "phase 3 + end barrier"]
+# mu_pass_bfw_kernel (wave tiles; per wave tile of 16 samples; slot 6 = the fold / loop overhead)
+NAMES_BFW = ["", "wait for the set", "stage + prefetch issue", "phase 1", "phase 2 + W' stores", "phase 3",
+             "fold + loop"]
 
 
 def main():
@@ -48,10 +51,11 @@ def main():
         tiles_per_wave = (plan.n_rows / 64) / plan.n_parts
         out = {"flags": flags, "waves": waves, "pass_us": round(pass_us, 2), "tiles_per_wave": round(tiles_per_wave, 2)}
         tot = 0
+        names = NAMES_BFW if os.environ.get("BFW", "1") == "1" else NAMES
         for i in range(1, 7):
             cyc = buf[i] / waves / tiles_per_wave
             tot += cyc
-            out[NAMES[i]] = round(cyc, 1)
+            out[names[i]] = round(cyc, 1)
         out["total_cycles_per_tile"] = round(tot, 1)
         out["implied_GHz"] = round(tot * tiles_per_wave / (pass_us * 1e3), 3)
         print(json.dumps(out), flush=True)

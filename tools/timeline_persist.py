@@ -136,21 +136,6 @@ def main():
     summary.update({"grid": g, "iters": a.iters, "launch_us": round(launch_us, 1),
                     "us_per_iter": round(launch_us / a.iters, 2),
                     "first_arrival_it0_us": round((arr[0].min() - t0) * 10 / 1e3, 2)})
-    if a.layout == 6:  # the reduce-scatter end: per iteration, from the last arrival
-        fr = lib.cnmf_debug_rs_timeline
-        fr.argtypes = [ctypes.c_void_p]
-        fr.restype = ctypes.c_int
-        rb = np.zeros(TL_IT * TL_WG * 3, dtype=np.uint64)
-        _lib.check(fr(rb.ctypes.data), "rs timeline")
-        rs = rb.reshape(TL_IT, TL_WG, 3).astype(np.int64)[1:n - 1, :g]
-        last = arr[1:n - 1].max(axis=1)[:, None]
-        ready = res[1:n - 1]
-        def q(v):
-            return [round(float(np.median(np.median(v, axis=1))) * 10 / 1e3, 2),
-                    round(float(np.median(v.max(axis=1))) * 10 / 1e3, 2)]
-        summary["rs_from_last_arrival_us_median_max"] = {
-            "rows_seen": q(rs[:, :, 0] - last), "columns_published": q(rs[:, :, 1] - last),
-            "ab_seen": q(rs[:, :, 2] - last), "basis_ready": q(ready - last)}
     if a.exchange:
         fx = lib.cnmf_debug_xtimeline
         fx.argtypes = [ctypes.c_void_p]

@@ -2212,6 +2212,92 @@ __device__ void basis_update_block(const double* AB, double* H64, double* Ht, do
     basis_update_small(AB, H64, Ht, HHt, F, k, KP, l1, l2, do_update, stats, lds);
 }
 
+// The basis update for KP = 16 (k = 9..16) spread over the 16-feature blocks of H: workgroup nb (one
+// wave) updates H[:, 16nb .. 16nb + 15] (den = (WᵀW)·H on v_mfma_f64_16x16x4_f64 in the arithmetic of
+// basis_update_mfma, SK:634-728), writes its H64 / Ht columns and its block's HHᵀ partial
+// Σ_f h[j][f]·h[m][f] (sc1 stores), takes a ticket, and the last arriver sums the partials in block
+// order into HHt (MI355X_MICROARCH.md "valid forms" row 1; one wave per workgroup, so the wave's own
+// vmcnt(0) covers every store the ticket signals).  The single-workgroup kernel ran 17.5 µs per cfg4
+// iteration on its serial phases (profiles/r03/bfw/bfw1/cfg4_kernel_stats.csv).
+__global__ __launch_bounds__(64) void basis_update_split_kernel(const double* __restrict__ AB, double* __restrict__ H64,
+                                                                double* __restrict__ Ht, double* __restrict__ HHt,
+                                                                int F, int k, double l1, double l2,
+                                                                double* __restrict__ scratch, uint32_t* ticket) {
+  typedef double f64x4v __attribute__((ext_vector_type(4)));
+  __shared__ double sh[16 * 17];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, li = lane & 15;
+  const int nb = blockIdx.x;
+  const int V = F + k;
+  const int f = 16 * nb + li;
+  const bool fok = f < F;
+  double bfr[4], hb[4], num[4], hold[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const int m = 4 * kk + g;
+    bfr[kk] = (li < k && m < k) ? AB[li * V + F + m] : 0.0;  // (WᵀW)[j = li][m]
+    hb[kk] = (m < k && fok) ? H64[m * F + f] : 0.0;           // H[m][f]
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = g + 4 * r;
+    const bool ok = j < k && fok;
+    num[r] = ok ? AB[j * V + f] : 0.0;   // (WᵀX)[j][f]
+    hold[r] = ok ? H64[j * F + f] : 0.0;
+  }
+  f64x4v den = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) den = __builtin_amdgcn_mfma_f64_16x16x4f64(bfr[kk], hb[kk], den, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int j = g + 4 * r;
+    double h = hold[r];
+    if (j < k && fok) {
+      double d = den[r];
+      if (l1 > 0.0) d += l1;          // SK:702-703
+      if (l2 > 0.0) d = d + l2 * h;   // SK:704-705
+      if (d == 0.0) d = EPS32;        // SK:706
+      h = h * (num[r] / d);           // SK:722-726
+      H64[j * F + f] = h;
+    }
+    if (fok) Ht[(size_t)f * 16 + j] = j < k ? h : 0.0;
+    sh[j * 17 + li] = (j < k && fok) ? h : 0.0;
+  }
+  // this block's HHᵀ partial: A[j = li][f = 4kk + g] = B[f][m = li] = h[li][4kk + g]
+  f64x4v hh = f64x4v{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const double v = sh[li * 17 + 4 * kk + g];
+    hh = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, hh, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)  // P[j = g + 4r][m = li]
+    __hip_atomic_store(scratch + ((size_t)nb * 16 + g + 4 * r) * 16 + li, hh[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint32_t old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0, 64);
+  if (old != gridDim.x - 1) return;
+  // the last arriver: HHᵀ = Σ_nb P_nb in block order (sc1 loads, all of a lane's in flight at once:
+  // the host keeps F <= 320, at most 20 blocks)
+  constexpr int NBM = 20;
+  double x[4][NBM];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int u = 0; u < NBM; ++u)
+      x[r][u] = __hip_atomic_load(scratch + (size_t)min(u, (int)gridDim.x - 1) * 256 + (g + 4 * r) * 16 + li,
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double v = 0.0;
+#pragma unroll
+    for (int u = 0; u < NBM; ++u) v += u < (int)gridDim.x ? x[r][u] : 0.0;
+    HHt[(g + 4 * r) * 16 + li] = v;
+  }
+  if (lane == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // at rest
+}
+
 __global__ __launch_bounds__(RED_NT) void basis_update_kernel(const double* __restrict__ AB,
                                                               double* __restrict__ H64,
                                                               double* __restrict__ Ht,
@@ -2268,6 +2354,7 @@ constexpr int DYN_GRP = 8;                       // workgroups per floating-tile
 constexpr int DYN_MAX_POOLS = sl::GROUP * sl::MAX_GROUPS / DYN_GRP;
 constexpr int CNT_POOL = CNT_ERR + 32;           // floating-tile pools [parity][pool] (32-word stride)
 constexpr int CNT_RCOL0 = CNT_POOL + 2 * DYN_MAX_POOLS * 32;          // reduce_kernel: one ticket per 64-column block
+constexpr int CNT_UPD = CNT_POOL;  // basis_update_split_kernel's ticket (the pools serve layout 3 only)
 constexpr int RED_MAX_COLS = 512;
 constexpr int CNT_WORDS = CNT_RCOL0 + RED_MAX_COLS;
 
@@ -6802,10 +6889,19 @@ int cnmf_reduce_update(const double* partials, int64_t n_parts, double* stage, u
   UpdateArgs ua{H64, Ht, HHt, n_features, k, padded_k(k), l1_H, l2_H, stats};
   if (ua.KP >= 8) {
     // k > 4: the reduction alone (small registers, full occupancy), then the matrix-core basis
-    // update as its own single-workgroup launch (its LDS stages the whole H)
+    // update: for KP = 16 spread over the 16-feature blocks of H (basis_update_split_kernel, the
+    // stage buffer free again as its scratch), else its own single-workgroup launch
     st = launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 0, ua,
                        reinterpret_cast<hipStream_t>(stream));
     if (st) return st;
+    if (ua.KP == 16 && !stats && n_features <= 320 &&
+        (int64_t)NSLICE * k * (n_features + k) >= 256 * ((n_features + 15) / 16)) {
+      hipLaunchKernelGGL(basis_update_split_kernel, dim3((unsigned)((n_features + 15) / 16)), dim3(64), 0,
+                         reinterpret_cast<hipStream_t>(stream), AB, H64, Ht, HHt, n_features, k, l1_H, l2_H, stage,
+                         counter + CNT_UPD);
+      HIP_CHECK(hipGetLastError());
+      return CNMF_OK;
+    }
     return cnmf_basis_update(AB, H64, Ht, HHt, n_features, k, l1_H, l2_H, 1, stats, stream);
   }
   return launch_reduce(partials, n_parts, k * (n_features + k), stage, counter, AB, 1, ua,

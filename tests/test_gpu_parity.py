@@ -249,3 +249,34 @@ def test_bf16_mfma_single_pass_matches_numpy(N, F, k):
     Wn = Wg.astype(np.float64)
     np.testing.assert_allclose(AB[:, :F], Wn.T @ Xr, rtol=2e-6)
     np.testing.assert_allclose(AB[:, F:], Wn.T @ Wn, rtol=2e-6)
+
+
+@pytest.mark.parametrize("k, F, dt", [(12, 100, "float32"), (16, 300, "bfloat16"), (9, 37, "float64")])
+def test_split_basis_update_iterations(k, F, dt):
+    """k = 9..16 (KP = 16): the basis update spread over H's 16-feature blocks
+    (basis_update_split_kernel, with the cross-block HHᵀ sum by the last arriver) inside the
+    per-iteration path; 40 iterations against the fp64 oracle (bf16: on the rounded X)."""
+    import torch
+    from cnmf_amd.solver import MUPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X32 = iop_spectra(30_000, F, seed=k + F, dtype=np.float32)
+    if dt == "bfloat16":
+        Xt = torch.from_numpy(X32).to(torch.bfloat16)
+    else:
+        Xt = torch.from_numpy(X32.astype(dt))
+    Xr = Xt.double().numpy()
+    W0, H0 = random_init(Xr.astype(np.float32), k, 42)
+    plan = MUPlan(Xt.cuda(), k)
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.iterate(40)
+    torch.cuda.synchronize()
+    Wr, Hr, _ = mu_ref.mu_fit(Xr, W0.astype(np.float64), H0.astype(np.float64), max_iter=40, tol=0.0)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    bar = 1e-9 if dt == "float64" else TOL32
+    assert rel_fro(W, Wr) <= bar and rel_fro(H, Hr) <= bar, (rel_fro(W, Wr), rel_fro(H, Hr))
+    Ht, HHt = plan.Ht.cpu().numpy(), plan.HHt.cpu().numpy()
+    np.testing.assert_array_equal(Ht[:, :k], H.T)
+    assert not Ht[:, k:].any() and not HHt[k:, :].any() and not HHt[:, k:].any()
+    np.testing.assert_allclose(HHt[:k, :k], H @ H.T, rtol=1e-12)
+    assert plan.counters_at_rest()

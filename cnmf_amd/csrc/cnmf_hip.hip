@@ -1142,7 +1142,7 @@ __host__ __device__ inline Lds lds(int F) {
   L.slotb = L.xbytes + TSW * 16 * 4;                   // + the wave tile's W [16][k <= 16] fp32
   L.slot = (int)align16((size_t)L.hht + 16 * 16 * 8);
   L.red = 2 * (NBX + 1) * 4 * 64 * 8;                  // end of launch: two waves' fp64 sums
-  const int loop = L.slot + 4 * L.slotb;
+  const int loop = L.slot + 8 * L.slotb;  // two wave-tile slots per wave
   L.total = loop > L.red ? loop : L.red;
   return L;
 }
@@ -1191,8 +1191,8 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   if (KC) k = KC;
   const int nchx = 2 * F, nchw = 4 * k;  // 16-byte chunks of a wave tile's X and W
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
-  unsigned char* xs = smem + L.slot + w * L.slotb;  // this wave's X tile [16][F] bf16 (+ zero pad)
-  const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);  // its W tile [16][k] fp32
+  // this wave's two slots (a pair of wave tiles per body): X tile [16][F] bf16 (+ zero pad), W [16][k]
+  unsigned char* xsp[2] = {smem + L.slot + (2 * w) * L.slotb, smem + L.slot + (2 * w + 1) * L.slotb};
 
   // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
   for (int e = t; e < bm::KP * 32 * KS; e += NT) {
@@ -1211,7 +1211,10 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   }
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = HHt[e];
-  if (l < 16) reinterpret_cast<uint32_t*>(xs + TSW * F * 2)[l] = 0u;  // the wave's zero pad
+  if (l < 16) {  // the slots' zero pads
+    reinterpret_cast<uint32_t*>(xsp[0] + TSW * F * 2)[l] = 0u;
+    reinterpret_cast<uint32_t*>(xsp[1] + TSW * F * 2)[l] = 0u;
+  }
   __syncthreads();
   double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li]
 #pragma unroll
@@ -1232,7 +1235,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
     for (int u = 0; u < PFX; ++u) ld16(pf[u], xsrc + 16 * (l + 64 * u < nchx ? l + 64 * u : l));
     ld16(pf[PFX], Wb + (size_t)r0 * k * 4 + 16 * (l < nchw ? l : 0));
   };
-  auto stage = [&](const u32x4 (&pf)[PFS]) {
+  auto stage = [&](const u32x4 (&pf)[PFS], unsigned char* xs) {
     stage_x<0>((unsigned)(uintptr_t)(xs + 16 * l), pf, l, nchx);
     if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * l), pf[PFX]);
   };
@@ -1243,38 +1246,46 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
 #pragma unroll
   for (int nb = 0; nb < NBX; ++nb) cacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   // invalid lanes' stores land in this workgroup's partial row (rewritten at the end of the launch;
-  // the host guarantees k(F+k) >= 512 doubles): every body issues exactly NSTB stores per lane
+  // the host guarantees k(F+k) >= 1024 doubles): every wave tile issues exactly NSTB stores per lane
   float* dummy = reinterpret_cast<float*>(partials + (size_t)blockIdx.x * k * (F + k)) + 64 * w + l;
   STAMP_DECL
 
-  auto body = [&](int i) {
-    const int64_t r0 = row0(i);
-    // phase 1: num for samples 4g + r, component li (16x16x32 bf16 against H's three terms)
-    double num64[4] = {0.0, 0.0, 0.0, 0.0};
-    {
-      const unsigned char* xa = xs + ((size_t)li * F + 8 * g) * 2;
-      const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
+  // phase 1 for a PAIR of wave tiles: each K-step's three H terms are read from LDS once for both
+  // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body)
+  auto phase1 = [&](double (&n0)[4], double (&n1)[4]) {
+    const unsigned char* xa0 = xsp[0] + ((size_t)li * F + 8 * g) * 2;
+    const unsigned char* xa1 = xsp[1] + ((size_t)li * F + 8 * g) * 2;
+    const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
 #pragma unroll
-      for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
-        if (!KSC && ks >= KS) break;
-        const uint64_t a0 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks);
-        const uint64_t a1 = *reinterpret_cast<const uint64_t*>(xa + 64 * ks + 8);
-        s16x8 a;
-        a.s0123 = __builtin_bit_cast(s16x4, a0);
-        a.s4567 = __builtin_bit_cast(s16x4, a1);
-        const s16x8 b1 = *reinterpret_cast<const s16x8*>(hb + 64 * ks);
-        const s16x8 b2 = *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks);
-        const s16x8 b3 = *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks);
-        const bf16x8 av = __builtin_bit_cast(bf16x8, a);
-        f32x4 num = f32x4{0.f, 0.f, 0.f, 0.f};
-        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b3), num, 0, 0, 0);
-        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b2), num, 0, 0, 0);
-        num = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b1), num, 0, 0, 0);
+    for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
+      if (!KSC && ks >= KS) break;
+      s16x8 a, c;
+      a.s0123 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa0 + 64 * ks));
+      a.s4567 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa0 + 64 * ks + 8));
+      c.s0123 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa1 + 64 * ks));
+      c.s4567 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa1 + 64 * ks + 8));
+      const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
+      const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
+      const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
+      const bf16x8 av = __builtin_bit_cast(bf16x8, a), cv = __builtin_bit_cast(bf16x8, c);
+      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f}, v = f32x4{0.f, 0.f, 0.f, 0.f};
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b2, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b2, v, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b1, v, 0, 0, 0);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) num64[r] += (double)num[r];
+      for (int r = 0; r < 4; ++r) {
+        n0[r] += (double)u[r];
+        n1[r] += (double)v[r];
       }
     }
-    STAMP(3);  // 3: phase 1
+  };
+  // phases 2 and 3 of one wave tile (slot p, first row r0; invalid: w' = 0 and dummy stores)
+  auto update = [&](int p, int64_t r0, bool valid, const double (&num64)[4]) {
+    const unsigned char* xs = xsp[p];
+    const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);
     // phase 2: den = w·HHᵀ (f64 MFMA; A row ρ = li carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is
     // sample 4g + r), then w' = w·num/den (SK:553-629) for (s = 4g + r, n = li)
     f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -1298,11 +1309,11 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
         if (d == 0.0) d = EPS32;            // SK:620
         wn = (float)(wold * (num64[r] / d));  // SK:622-629
       }
+      wn = valid ? wn : 0.f;
       wr[r] = wn;
-      float* dst = li < k ? W + (size_t)(r0 + s) * k + li : dummy + 256 * r;
+      float* dst = (valid && li < k) ? W + (size_t)(r0 + s) * k + li : dummy + 256 * (r + 4 * p);
       *dst = wn;
     }
-    STAMP(4);  // 4: phase 2 (+ the W' stores)
     if (!do_acc) return;
     // phase 3: A[m = 4g + r][f = 16nb + li] and B[m][n] over the tile's 16 samples
     s16x4 a1, a2, a3;  // w'[4g + j][li] in three bf16 terms: the A operand (row m = li, k = 4g + j)
@@ -1318,8 +1329,8 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
-    const int q = li >> 2, p = li & 3;
-    const unsigned char* xb0 = xs + ((size_t)(4 * g + q) * F + 4 * p) * 2;
+    const int q = li >> 2, pp = li & 3;
+    const unsigned char* xb0 = xs + ((size_t)(4 * g + q) * F + 4 * pp) * 2;
 #pragma unroll
     for (int nb = 0; nb < NBX; ++nb) {
       if (nb < (KSC ? 2 * KSC : NB)) {
@@ -1329,31 +1340,33 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
         cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, b, cacc[nb], 0, 0, 0);
       }
     }
-    STAMP(5);  // 5: phase 3
   };
 
   u32x4 pf[PD][PFS];
+  static_assert(PD == 2, "a pair of wave tiles per body");
+  prefetch(pf[0], 0);
+  prefetch(pf[1], 1);
 #pragma unroll
-  for (int s0 = 0; s0 < PD; ++s0) {
-    prefetch(pf[s0], s0);
-#pragma unroll
-    for (int d = 0; d < NSTB; ++d) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy + 256 * d), "v"(0) : "memory");
-  }
-  int nx = PD;
-  for (int i0 = 0; i0 < ntw; i0 += PD) {
-#pragma unroll
-    for (int s0 = 0; s0 < PD; ++s0) {
-      STAMP(0);
-      // younger than this set: the PD - 1 later sets and the stores of the PD bodies since
-      wait_set<PFS * (PD - 1) + NSTB * PD>(pf[s0]);
-      STAMP(1);  // 1: wait for the set
-      stage(pf[s0]);
-      prefetch(pf[s0], nx);
-      ++nx;
-      STAMP(2);  // 2: stage + prefetch issue
-      if (i0 + s0 < ntw) body(i0 + s0);
-      STAMP(6);  // 6: the fold (every QF tiles) and the loop
-    }
+  for (int d = 0; d < 2 * NSTB; ++d)  // as if a body had run: the first waits count exactly
+    asm volatile("global_store_dword %0, %1, off" ::"v"(dummy + 256 * d), "v"(0) : "memory");
+  for (int i0 = 0; i0 < ntw; i0 += 2) {
+    STAMP(0);
+    // younger than set 0: set 1's loads and the previous body's 2·NSTB stores; than set 1: the stores
+    wait_set<PFS + 2 * NSTB>(pf[0]);
+    stage(pf[0], xsp[0]);
+    wait_set<2 * NSTB>(pf[1]);
+    stage(pf[1], xsp[1]);
+    STAMP(1);  // 1: waits + staging
+    prefetch(pf[0], i0 + 2);
+    prefetch(pf[1], i0 + 3);
+    STAMP(2);  // 2: prefetch issue
+    double n0[4] = {0.0, 0.0, 0.0, 0.0}, n1[4] = {0.0, 0.0, 0.0, 0.0};
+    phase1(n0, n1);
+    STAMP(3);  // 3: phase 1 (both tiles)
+    update(0, row0(i0), true, n0);
+    STAMP(4);  // 4: phases 2 + 3 of the first tile
+    update(1, row0(i0 + 1), i0 + 1 < ntw, n1);
+    STAMP(5);  // 5: phases 2 + 3 of the second tile
   }
   STAMP_FLUSH;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
@@ -5166,7 +5179,7 @@ static bool use_bf16_mfma(int x_dtype, int F, int k) {
 static bool g_no_bfw = diag_env("CNMF_BFW") && atoi(diag_env("CNMF_BFW")) == 0;
 static bool use_bfw(int x_dtype, int F, int k) {
   return !g_no_bfw && !g_force_valu && use_bf16_mfma(x_dtype, F, k) && F >= 8 && F <= 16 * bw::NBX &&
-         k * (F + k) >= 512 && bw::lds(F).total <= (int)kMaxLds;
+         k * (F + k) >= 1024 && bw::lds(F).total <= (int)kMaxLds;
 }
 static PassFn bfw_fn(int F, int k) {
   return (bm::ksteps(F) == 10 && k == 16) ? reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<10, 16>)

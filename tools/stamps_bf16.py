@@ -13,9 +13,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 NAMES = ["", "stage wait+LDS write", "staging barrier", "prefetch issue", "phase 1", "phase 2 + barrier",
          "phase 3 + end barrier"]
-# mu_pass_bfw_kernel (wave tiles; per wave tile of 16 samples; slot 6 = the fold / loop overhead)
-NAMES_BFW = ["", "wait for the set", "stage + prefetch issue", "phase 1", "phase 2 + W' stores", "phase 3",
-             "fold + loop"]
+# mu_pass_bfw_kernel (wave tiles, a pair per body; cycles per wave tile of 16 samples)
+NAMES_BFW = ["", "waits + staging", "prefetch issue", "phase 1 (the pair)", "phases 2+3, first tile",
+             "phases 2+3, second tile", "-"]
 
 
 def main():

@@ -97,3 +97,22 @@ def test_run_mu_takes_the_device_path_and_falls_back():
         n2 = run_mu(plan2, max_iter=300, tol=1e-4)
     assert n2 == nr and not plan2.persistent and plan2.counters_at_rest()
     assert rel_fro(plan2.W.cpu().numpy(), Wr) <= 1e-5 and rel_fro(plan2.H64.cpu().numpy(), Hr) <= 1e-5
+
+
+@pytest.mark.parametrize("n,k", [(64 * 3000, 4), (1_200_000, 8)])
+def test_device_tol_without_a_stop_is_bit_identical(n, k):
+    """A fit whose tolerance never triggers runs the same arithmetic as the plain persistent launch:
+    W and H bit for bit (the TOL kernel's extra loss column, snapshot stores and counted waits change
+    nothing else; k = 8 at 1.2e6 rows streams W)."""
+    import torch
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(n, 81, seed=5, dtype=np.float32)
+    W0, H0 = random_init(X, k, 3)
+    a, b = _plan(X, W0, H0), _plan(X, W0, H0)
+    res = a.fit_device_tol(120, 1e-14)
+    assert res is not None and res[0] == 120
+    b.iterate(120)
+    torch.cuda.synchronize()
+    a.check_sync_error()
+    b.check_sync_error()
+    assert torch.equal(a.W, b.W) and torch.equal(a.H64, b.H64)

@@ -4657,6 +4657,15 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     double* vz = e2 + 4 * F;  // the block form's L0, L1, L2 are not used here
     int* idx = reinterpret_cast<int*>(vz + F) + 2 * F;
     const uint64_t lt = (1ull << lane) - 1ull;
+    // λ·(DᵀD) entries of the lane's two features: the same for every row of the sweep
+    double ld0[2], le1[2], le2[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int f = lane + 64 * c;
+      ld0[c] = f < F ? lam * als_L_entry(F, f, f) : 0.0;
+      le1[c] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
+      le2[c] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
+    }
     for (int j = 0; j < k; ++j) {
       const double bjj = sB[j * k + j];
       if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
@@ -4676,9 +4685,9 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           for (int m = 0; m < k; ++m)
             if (m != j) b -= sB[j * k + m] * sH[m * F + f];
           rb[c] = b;
-          rd[c] = bjj + lam * als_L_entry(F, f, f);
-          re1[c] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
-          re2[c] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
+          rd[c] = bjj + ld0[c];
+          re1[c] = le1[c];
+          re2[c] = le2[c];
           pas[c] = sH[j * F + f] > 0.0;
           vb[f] = rb[c];
           d0[f] = rd[c];

@@ -93,6 +93,7 @@ struct bf16_t {
 
 // native 16-byte vector (HIP's uint4 class type defeats SROA: the prefetch array went to scratch)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float to_c(float v) { return v; }
 __device__ __forceinline__ double to_c(double v) { return v; }
@@ -1131,14 +1132,24 @@ constexpr int PD = 2;         // wave tiles in flight per wave
 constexpr int NBX = 20;       // 16-feature blocks (F <= 320)
 constexpr int NSTB = 4;       // global stores per body (the lane's four w')
 struct Lds {
-  int hs, hrow, hht, slot, xbytes, slotb, red, total;
+  int hs, hrow, hht, slot, xrow, xbytes, slotb, red, total;
 };
+// X row stride in a slot: the least multiple of 32 bytes >= 2F with an odd quotient (≡ 32, 96, 160 or
+// 224 mod 256: 608 at F = 300).  Row ρ then starts on dword 8·odd·ρ mod 64, so phase 1's ds_read_b128
+// row reads (rows li, 16-B columns g: groups of 16 lanes) and phase 3's transposed reads (rows 4g + q,
+// 8-B columns pp) fall on distinct banks; the packed 600-B rows were 2- and 3-way conflicted.
+__host__ __device__ inline int xrow_stride(int F) {
+  int r = (2 * F + 31) / 32;
+  if ((r & 1) == 0) ++r;
+  return 32 * r;
+}
 __host__ __device__ inline Lds lds(int F) {
   Lds L;
-  L.hrow = (32 * bm::ksteps(F) + 8) * 2;                // H split rows (bm's conflict-free stride)
+  L.hrow = xrow_stride(32 * bm::ksteps(F));            // H split rows: the same rule, for the b128 reads
   L.hs = 0;
   L.hht = L.hs + 3 * bm::KP * L.hrow;
-  L.xbytes = (int)align16((size_t)TSW * F * 2 + 64);   // + 64 zero bytes for the reads past the last row
+  L.xrow = xrow_stride(F);
+  L.xbytes = (int)align16((size_t)TSW * L.xrow + 64);  // + 64 zero bytes for the reads past the last row
   L.slotb = L.xbytes + TSW * 16 * 4;                   // + the wave tile's W [16][k <= 16] fp32
   L.slot = (int)align16((size_t)L.hht + 16 * 16 * 8);
   L.red = 2 * (NBX + 1) * 4 * 64 * 8;                  // end of launch: two waves' fp64 sums
@@ -1161,10 +1172,21 @@ template <int OFF>
 __device__ __forceinline__ void st16(unsigned addr, const u32x4& v) {
   asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(addr), "a"(v), "i"(OFF) : "memory");
 }
+__device__ __forceinline__ void st8(unsigned addr, const u32x2& v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"(addr), "a"(v) : "memory");
+}
+// chunk U of the lane (tile bytes o = 16(l + 64U) .. o + 15) into the padded rows: each 8-byte half
+// lies in one row (2F ≡ 0 mod 8); row = o / 2F by a multiply-high (mrow = ⌈2^32 / 2F⌉, exact for
+// o < 2^16), LDS byte = o + pad·row
 template <int U>
-__device__ __forceinline__ void stage_x(unsigned addr, const u32x4* pf, int l, int nch) {
-  if (l + 64 * U < nch) st16<1024 * U>(addr, pf[U]);
-  if constexpr (U + 1 < PFX) stage_x<U + 1>(addr, pf, l, nch);
+__device__ __forceinline__ void stage_x(unsigned base, const u32x4* pf, int l, int nch, unsigned mrow,
+                                        unsigned pad) {
+  if (l + 64 * U < nch) {
+    const unsigned o = 16u * (unsigned)(l + 64 * U);
+    st8(base + o + pad * __umulhi(o, mrow), u32x2{pf[U][0], pf[U][1]});
+    st8(base + o + 8u + pad * __umulhi(o + 8u, mrow), u32x2{pf[U][2], pf[U][3]});
+  }
+  if constexpr (U + 1 < PFX) stage_x<U + 1>(base, pf, l, nch, mrow, pad);
 }
 }  // namespace bw
 
@@ -1193,6 +1215,8 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
   // this wave's two slots (a pair of wave tiles per body): X tile [16][F] bf16 (+ zero pad), W [16][k]
   unsigned char* xsp[2] = {smem + L.slot + (2 * w) * L.slotb, smem + L.slot + (2 * w + 1) * L.slotb};
+  const int XR = L.xrow;
+  const unsigned xpad = (unsigned)(XR - 2 * F), mrow = (unsigned)((0x100000000ull + 2 * F - 1) / (2 * F));
 
   // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
   for (int e = t; e < bm::KP * 32 * KS; e += NT) {
@@ -1211,9 +1235,14 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   }
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = HHt[e];
-  if (l < 16) {  // the slots' zero pads
-    reinterpret_cast<uint32_t*>(xsp[0] + TSW * F * 2)[l] = 0u;
-    reinterpret_cast<uint32_t*>(xsp[1] + TSW * F * 2)[l] = 0u;
+  if (l < 16) {  // the slots' zero pads: past the last row, and (never staged) each row's tail
+    reinterpret_cast<uint32_t*>(xsp[0] + TSW * XR)[l] = 0u;
+    reinterpret_cast<uint32_t*>(xsp[1] + TSW * XR)[l] = 0u;
+  }
+  for (int e = l; e < TSW * (int)(xpad / 4); e += 64) {
+    const int r = e / (int)(xpad / 4), c = e - r * (int)(xpad / 4);
+    reinterpret_cast<uint32_t*>(xsp[0] + r * XR + 2 * F)[c] = 0u;
+    reinterpret_cast<uint32_t*>(xsp[1] + r * XR + 2 * F)[c] = 0u;
   }
   __syncthreads();
   double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li]
@@ -1236,8 +1265,11 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
     ld16(pf[PFX], Wb + (size_t)r0 * k * 4 + 16 * (l < nchw ? l : 0));
   };
   auto stage = [&](const u32x4 (&pf)[PFS], unsigned char* xs) {
-    stage_x<0>((unsigned)(uintptr_t)(xs + 16 * l), pf, l, nchx);
-    if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * l), pf[PFX]);
+    stage_x<0>((unsigned)(uintptr_t)xs, pf, l, nchx, mrow, xpad);
+    // W [16][k]: at k = 16 the lane's chunk (s = l/4, j = l%4) goes to chunk j ^ ((s >> 1) & 3) of row s,
+    // so phase 2's column reads (16 samples × 2 components per half-wave) spread over 16 banks, not 4
+    const int wch = KC == 16 ? (l & ~3) | ((l & 3) ^ ((l >> 3) & 3)) : l;
+    if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * wch), pf[PFX]);
   };
 
   // accumulators: phase 3's fp32 MFMA chains over the wave's tiles (in AGPRs: no VALU touches
@@ -1253,17 +1285,14 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   // phase 1 for a PAIR of wave tiles: each K-step's three H terms are read from LDS once for both
   // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body)
   auto phase1 = [&](double (&n0)[4], double (&n1)[4]) {
-    const unsigned char* xa0 = xsp[0] + ((size_t)li * F + 8 * g) * 2;
-    const unsigned char* xa1 = xsp[1] + ((size_t)li * F + 8 * g) * 2;
+    const unsigned char* xa0 = xsp[0] + li * XR + 16 * g;
+    const unsigned char* xa1 = xsp[1] + li * XR + 16 * g;
     const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
 #pragma unroll
     for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
       if (!KSC && ks >= KS) break;
-      s16x8 a, c;
-      a.s0123 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa0 + 64 * ks));
-      a.s4567 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa0 + 64 * ks + 8));
-      c.s0123 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa1 + 64 * ks));
-      c.s4567 = __builtin_bit_cast(s16x4, *reinterpret_cast<const uint64_t*>(xa1 + 64 * ks + 8));
+      const s16x8 a = *reinterpret_cast<const s16x8*>(xa0 + 64 * ks);  // 16-B aligned rows: one b128
+      const s16x8 c = *reinterpret_cast<const s16x8*>(xa1 + 64 * ks);
       const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
       const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
       const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
@@ -1286,6 +1315,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   auto update = [&](int p, int64_t r0, bool valid, const double (&num64)[4]) {
     const unsigned char* xs = xsp[p];
     const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);
+    auto wix = [&](int s, int m) { return KC == 16 ? 16 * s + (m ^ (((s >> 1) & 3) << 2)) : s * k + m; };
     // phase 2: den = w·HHᵀ (f64 MFMA; A row ρ = li carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is
     // sample 4g + r), then w' = w·num/den (SK:553-629) for (s = 4g + r, n = li)
     f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
@@ -1293,7 +1323,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int m = 4 * kk + g;
-      const double av = m < k ? (double)wso[sa * k + m] : 0.0;
+      const double av = m < k ? (double)wso[wix(sa, m)] : 0.0;
       den = __builtin_amdgcn_mfma_f64_16x16x4f64(av, hhb[kk], den, 0, 0, 0);
     }
     float wr[4];
@@ -1303,7 +1333,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
       float wn = 0.f;
       if (li < k) {
         double d = den[r];
-        const double wold = (double)wso[s * k + li];
+        const double wold = (double)wso[wix(s, li)];
         if (l1 > 0.0) d += l1;              // SK:616-617
         if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
         if (d == 0.0) d = EPS32;            // SK:620
@@ -1330,7 +1360,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
 #pragma unroll
     for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
     const int q = li >> 2, pp = li & 3;
-    const unsigned char* xb0 = xs + ((size_t)(4 * g + q) * F + 4 * pp) * 2;
+    const unsigned char* xb0 = xs + (4 * g + q) * XR + 8 * pp;
 #pragma unroll
     for (int nb = 0; nb < NBX; ++nb) {
       if (nb < (KSC ? 2 * KSC : NB)) {

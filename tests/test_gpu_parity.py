@@ -221,13 +221,16 @@ def test_factorise_normalise_option():
 
 
 @pytest.mark.parametrize("N, F, k", [(4096 + 29, 300, 16), (1000, 64, 12), (777, 300, 9), (3000, 124, 16),
-                                     (64 * 700, 300, 16), (40, 300, 16), (64 * 1000 + 16, 320, 13)])
+                                     (64 * 700, 300, 16), (40, 300, 16), (64 * 1000 + 16, 320, 13),
+                                     # the wave-tile slot's X row stride (§3.4): 2F already at the
+                                     # stride (F = 48: no pad), the widest pad (F = 52: 56 B), k < 16
+                                     (64 * 50 + 7, 48, 16), (64 * 30, 52, 16), (64 * 40 + 33, 96, 11)])
 def test_bf16_mfma_single_pass_matches_numpy(N, F, k):
     """§8 a8: the bf16 matrix-core pass (the wave-tile mu_pass_bfw_kernel over the full 64-sample
     tiles, the 64-sample mu_pass_bf16_mfma_kernel on a ragged tail: v_mfma_f32_16x16x32 /
     16x16x16 bf16 with 3-term bf16 splits of H and W', ds_read_b64_tr_b16 column reads): one W
     update and [WᵀX | WᵀW] vs NumPy fp64 on the bf16-rounded X (ragged last tile, no full tile at
-    all, whole tiles only, k < 16 padding, F = 320)."""
+    all, whole tiles only, k < 16 padding, F = 320, padded and unpadded LDS rows)."""
     import torch
     from cnmf_amd.solver import MUPlan
     from cnmf_amd import _lib

@@ -75,6 +75,11 @@ def parse():
                    help="untimed clock ramp after the warmup: iterations on copies of W and H until "
                         "this much GPU time has passed (the chip holds a low clock for its first "
                         "tens of ms of work; the state is restored, the timed K steps are unchanged)")
+    p.add_argument("--settle-ms", type=float, default=2.0,
+                   help="idle pause (ms) between the last untimed launch and the timed region: right "
+                        "behind a busy launch a short timed launch reads up to 13 %% slower, after a "
+                        "1-300 ms pause it reads the steady 500-step rate (tools/driver_form_probe.py, "
+                        "DESIGN §5)")
     p.add_argument("--no-tune", action="store_true",
                    help="skip timing the persistent-launch layouts (MUPlan.tune) before the run")
     p.add_argument("--layout", type=int, default=0,
@@ -127,8 +132,11 @@ def _time_oracle_mu(X, W0, H0, budget_s):
 
 def cpu_baseline(X, W0, H0, budget_s):
     """Oracle fp32 MU iterations (SK:526-728 arithmetic via oracle/mu_ref.py) on the host cores:
-    with the BLAS threads the process has (os.cpu_count()-bounded, reported as `cores`) and with ONE
-    thread; the CPU model and BLAS vendor are named."""
+    with the BLAS threads this process is granted (reported as `cores`) and with ONE thread (SURVEY
+    §8(d)); the CPU model and BLAS vendor are named.  SURVEY §8(d) asks for os.cpu_count() threads;
+    on the GPU box os.cpu_count() counts the whole machine (256 logical CPUs) while one GPU's job is
+    granted a 16-CPU share (OMP_NUM_THREADS=16, which the box's rules say to leave as set), so the
+    granted share is what is used and `cpu_share` says so."""
     try:
         from threadpoolctl import threadpool_info, threadpool_limits
         info = threadpool_info()
@@ -149,7 +157,10 @@ def cpu_baseline(X, W0, H0, budget_s):
                       f"NumPy fp32 ({blas} BLAS, {threads} threads), on the same "
                       f"{X.shape[0]}x{X.shape[1]} k={W0.shape[1]} X as the GPU run",
             "seconds": round(el, 3), "cpu_model": cpu_model(), "logical_cpus": os.cpu_count(),
-            "blas": blas, "one_thread": one_thread}
+            "blas": blas, "one_thread": one_thread,
+            "cpu_share": (f"{threads} BLAS threads = the CPU share granted to this job "
+                          f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}); "
+                          f"os.cpu_count() = {os.cpu_count()} counts the whole host")}
 
 
 def cpu_baseline_als(X, W0, H0, delta, lam, budget_s):
@@ -290,9 +301,50 @@ def load_traffic(path, n_rows, F, k):
     return per_it, ent.get("source")
 
 
+def launcher_decision(gpus: int, env, device_count: int, backend: str):
+    """How `bench.py --gpus N` runs (never time one rank and call it N):
+    ("run", None) — this process is a rank of a world of exactly N (a launcher set WORLD_SIZE = N, or
+    N = 1 without one); ("spawn", None) — no launcher and N > 1: start N ranks as children through
+    torch.distributed.run; ("refuse", why) — WORLD_SIZE disagrees with --gpus, or RCCL would need
+    more devices than are visible."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "refuse", (f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks: the line would "
+                              f"report the wrong GPU count")
+        return "run", None
+    if gpus <= 1:
+        return "run", None
+    if backend == "nccl" and device_count < gpus:
+        return "refuse", (f"--gpus {gpus} needs {gpus} visible devices for RCCL, {device_count} visible "
+                          f"(--backend gloo lets ranks share a device)")
+    return "spawn", None
+
+
+def spawn_ranks(gpus: int) -> int:
+    """Start `gpus` ranks of this script through torch.distributed.run (one process per GPU, the
+    driver's own launch line) from this parent, which never touches the GPU; returns their exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"[bench] no launcher: starting {gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
 def main():
     args = parse()
     import torch
+    # decided before any HIP call (device_count does not initialise the runtime on this image)
+    how, why = launcher_decision(args.gpus, os.environ, torch.cuda.device_count(), args.backend)
+    if how == "refuse":
+        print(f"[bench] refused: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if how == "spawn":
+        sys.exit(spawn_ranks(args.gpus))
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -422,6 +474,8 @@ def main():
         else:
             run = plan.prepare(K, pass_events=events)
         torch.cuda.synchronize()
+        if args.settle_ms > 0:
+            time.sleep(args.settle_ms / 1e3)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()

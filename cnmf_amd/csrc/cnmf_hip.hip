@@ -6611,7 +6611,7 @@ static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy
 
 extern "C" {
 
-int cnmf_abi_version(void) { return 300; }
+int cnmf_abi_version(void) { return 301; }
 
 const char* cnmf_last_error(void) { return g_err; }
 
@@ -7006,6 +7006,13 @@ static bool g_no_persist = diag_env("CNMF_PERSIST") && strcmp(diag_env("CNMF_PER
 // prefetch depth of the persistent kernel (CNMF_PERSIST_PD=1|2); CNMF_WRES=0 keeps W streaming
 static int g_persist_pd = (diag_env("CNMF_PERSIST_PD") && atoi(diag_env("CNMF_PERSIST_PD")) == 1) ? 1 : 2;
 static bool g_no_wres = diag_env("CNMF_WRES") && strcmp(diag_env("CNMF_WRES"), "0") == 0;
+// The round-1 workgroup-tile kernel (mu_iter_sl_kernel: layouts 1 pairs, 2 teams, 3 floating tiles,
+// DESIGN §3.0b) is instantiated in the diagnostic build only: the wave tiles (layout 4) won on every
+// box, and layout 3 is not bit-repeatable (housekeeping).  In the product its launch
+// functions are null and persist_grid() is 0, so every persistent launch is a wave-tile one.
+#ifndef CNMF_DIAG
+static PassFn persist_fn(bool = false, bool = false) { return nullptr; }
+#else
 static PassFn persist_fn(bool wres = false, bool multi = false) {
   if (multi)  // the multi-GPU launch: PD = 2 only
     return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true>)
@@ -7014,8 +7021,10 @@ static PassFn persist_fn(bool wres = false, bool multi = false) {
     return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<1, false>);
   return wres ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true>) : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, false>);
 }
+#endif
 
 static int64_t persist_grid(int64_t n_rows, int x_dtype, int F, int k, bool multi = false) {
+  if (!persist_fn(false, multi)) return 0;  // the product build: wave tiles only
   if (g_no_persist || !use_sl(x_dtype, F, k) || n_rows % TS != 0) return 0;
   const int64_t n_tiles = n_rows / TS;
   const int min_tiles = g_persist_pd + 2;  // per workgroup (the W re-read hazard, see the kernel)
@@ -7049,24 +7058,36 @@ static size_t persist_wres_lds(int64_t n_rows, int64_t G, bool multi = false) {
 // of 4 / 1 / 2 is fastest has differed between boxes, so MUPlan.tune() times them and keeps the
 // fastest for its plan.  0 = the default (4; CNMF_PERSIST_VARIANT / CNMF_TEAMS in the diagnostic build).
 static int default_layout() {
+#ifndef CNMF_DIAG
+  return 4;
+#endif
   const char* v = diag_env("CNMF_PERSIST_VARIANT");
   if (v && atoi(v) >= 1 && atoi(v) <= 4) return atoi(v);
   return (diag_env("CNMF_TEAMS") && strcmp(diag_env("CNMF_TEAMS"), "2") == 0) ? 2 : 4;
 }
 static int resolve_layout(int layout) {
   if (layout == 0) return default_layout();
+#ifdef CNMF_DIAG
   return (layout >= 1 && layout <= 5) ? layout : -1;
+#else
+  return (layout == 4 || layout == 5) ? layout : -1;
+#endif
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
-      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 1 (pairs), 2 (teams), 3 (floating tiles), " \
-                     "4 (wave tiles) or 5 (k = 8 wave tiles on the matrix cores)");                       \
+      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 4 (wave tiles) or 5 (k = 8 wave tiles on "  \
+                     "the matrix cores); 1-3 are in the diagnostic build only");                          \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
+#ifndef CNMF_DIAG
+  (void)multi;
+  return nullptr;
+#else
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 2>)
                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 2>);
+#endif
 }
 
 // ---- variant 3: pairs with floating tiles (mu_iter_sl_kernel<2, true, MULTI, 1, true>): each
@@ -7081,8 +7102,13 @@ static double dyn_frac() {
 }
 static bool g_dyn_multi = diag_env("CNMF_DYN_MULTI") && strcmp(diag_env("CNMF_DYN_MULTI"), "1") == 0;
 static PassFn persist_dyn_fn(bool multi) {
+#ifndef CNMF_DIAG
+  (void)multi;
+  return nullptr;
+#else
   return multi ? reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, true, 1, true>)
                : reinterpret_cast<PassFn>(&mu_iter_sl_kernel<2, true, false, 1, true>);
+#endif
 }
 static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, int layout, size_t* lds_out) {
   if (layout != 3 || g_no_wres || g_persist_pd != 2 || G <= 0) return 0;
@@ -7092,7 +7118,7 @@ static int persist_dyn_static(int64_t n_tiles, int64_t G, bool multi, int layout
   if (S < 4 || S * G > n_tiles) return 0;  // >= PD + 2 static tiles (no draw crosses an iteration)
   const size_t lds = (size_t)sl::L_PTOTAL + (size_t)S * sl::WB;
   if (lds > kMaxLds) return 0;
-  if (max_resident(persist_dyn_fn(multi), lds) < G) return 0;  // the whole grid co-resident
+  if (!persist_dyn_fn(multi) || max_resident(persist_dyn_fn(multi), lds) < G) return 0;  // the whole grid co-resident
   *lds_out = lds;
   return (int)S;
 }
@@ -7109,6 +7135,7 @@ static int64_t persist_teams_grid(int64_t n_tiles, bool multi, int layout, size_
   const size_t lds = 2 * ((size_t)sl::L_PTOTAL + (size_t)nbt_max * sl::WB);
   if (lds > kMaxLds) return 0;
   const PassFn fn = persist_teams_fn(multi);
+  if (!fn) return 0;
   if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 2 * NT, lds) != hipSuccess) return 0;
@@ -7358,8 +7385,10 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
 int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int layout, int multi) {
   RESOLVE_LAYOUT(layout);
   WtLaunch L;
-  if (wt_plan(n_rows, x_dtype, n_features, k, multi != 0, layout, &L)) return L.G;
-  const int64_t g = persist_grid(n_rows, x_dtype, n_features, k, multi != 0);
+  // multi: bit 0 = the in-launch exchange form, bit 1 = the device tolerance test's (TOL) kernel
+  if (wt_plan(n_rows, x_dtype, n_features, k, (multi & 1) != 0, layout, &L, (multi & 2) != 0)) return L.G;
+  if (multi & 2) return 0;  // cnmf_mu_fit_tol serves the wave tiles only
+  const int64_t g = persist_grid(n_rows, x_dtype, n_features, k, (multi & 1) != 0);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : g;
 }
 

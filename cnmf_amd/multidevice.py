@@ -55,6 +55,11 @@ class LocalGroup:
     def abort(self):
         self._barrier.abort()
 
+    def reset(self):
+        """Make the group usable again after an abort (call once every thread has left it)."""
+        self._barrier.reset()
+        self._slots = [None] * self._size
+
     def _exchange(self, rank: int, obj):
         self._slots[rank] = obj
         self._barrier.wait()
@@ -164,6 +169,8 @@ class MultiDeviceFit:
             t.start()
         for t in threads:
             t.join()
+        if any(errs):  # every thread has left the rendezvous: the group serves the fallback path
+            self.group.reset()
         first = [e for e in errs if e is not None and not isinstance(e, threading.BrokenBarrierError)]
         if first or any(errs):
             raise first[0] if first else errs[0]

@@ -16,7 +16,6 @@ SK:<line> = sklearn/decomposition/_nmf.py (1.7.2).
 from __future__ import annotations
 
 import ctypes
-import os
 import math
 
 import torch
@@ -434,11 +433,11 @@ class MUPlan:
             self._allreduce(self.AB)
         self.basis_update()
 
-    def tune(self, n_iter: int = 100, rounds: int = 2, variants=(4, 1, 2)) -> dict:
+    def tune(self, n_iter: int = 100, rounds: int = 2, variants=None) -> dict:
         """Time the layouts of the persistent launch (the `layout` argument, include/cnmf_hip.h:
-        4 = wave tiles, 1 = pairs of 4-wave workgroups, 2 = 8-wave two-team workgroups; 3 = pairs
-        with floating tiles is not bit-repeatable and only timed when asked for) on this plan's
-        shape and keep the fastest for THIS plan.  Runs on copies of W and H: the plan's state is
+        at k = 8, 4 = the VALU wave tiles and 5 = the matrix-core wave tiles; k = 4 has one layout in
+        the product library, so there is nothing to time unless `variants` names some) on this
+        plan's shape and keep the fastest for THIS plan.  Runs on copies of W and H: the plan's state is
         unchanged.  Collective over the plan's group: every rank times the same launches in the
         same order, the per-layout times are max-reduced over the ranks and every rank keeps the
         same layout (the ranks' launches must match: the in-launch exchange, and the shard steps'
@@ -447,8 +446,10 @@ class MUPlan:
         (empty dict) for non-persistent plans."""
         if not self.persistent or self.k not in (4, 8) or self.xdt != _lib.F32:
             return {}  # the layouts are alternatives for fp32 k = 4 and k = 8 only
-        if self.k == 8:  # k = 8: the VALU wave tiles (4) or the matrix-core wave tiles (5)
-            variants = (4, 5)
+        if variants is None:  # k = 8: the VALU wave tiles (4) or the matrix-core wave tiles (5)
+            variants = (4, 5) if self.k == 8 else (4,)
+        if len(variants) < 2:
+            return {}
         W0, H0 = self.W.clone(), self.H64.clone()
         keep = self.layout
         times = {v: [] for v in variants}
@@ -489,8 +490,20 @@ class MUPlan:
         checked), restoring W from the snapshot when the test stopped a streamed-W fit.  None when
         the library does not serve this plan's shape (the caller runs the host loop)."""
         import numpy as np
-        if not self.persistent or self.n_rows == 0 or tol <= 0 or max_iter <= 0:
+        if not self.persistent or tol <= 0 or max_iter <= 0:  # the same on every rank
             return None
+        xctl = _ptr(self.xctl) if getattr(self, "exchange", False) else None
+        # this shard's eligibility, asked of the TOL kernel's own plan (bit 1), then agreed over the
+        # plan's group (ADVICE r3): ranks that launched the exchange-plus-tol kernel would wait in
+        # the exchange for a rank that took the host loop
+        with torch.cuda.device(self.device):
+            probe = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, self.layout,
+                                                     (1 if xctl is not None else 0) | 2)
+        ok = self.n_rows > 0 and probe > 0 and "wave tiles" in self.describe()
+        if self.world > 1 and agree_max([0.0 if ok else 1.0], self.group, self.device)[0] != 0.0:
+            return None
+        if not ok:
+            return None  # not a wave-tile shape / layout: the host loop
         n_tc = int(check(self.lib.cnmf_tolctl_doubles(max_iter), "cnmf_tolctl_doubles"))
         if self._wsnap is None or self._wsnap.shape != self.W.shape:
             self._wsnap = torch.empty_like(self.W)
@@ -499,7 +512,6 @@ class MUPlan:
         host[self._TC["cap"]] = n_tc - self._TC["errs"]
         host[self._TC["wsnap"]] = np.array([self._wsnap.data_ptr()], dtype=np.uint64).view(np.float64)[0]
         tolctl = torch.from_numpy(host).to(self.device)
-        xctl = _ptr(self.xctl) if getattr(self, "exchange", False) else None
         args = (max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
                 _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self._AB),
                 _ptr(tolctl), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H,
@@ -507,11 +519,6 @@ class MUPlan:
         fn = self.lib.cnmf_mu_fit_tol
         cargs = tuple(None if a is None else t(a) if not isinstance(a, ctypes.Array) else a
                       for a, t in zip(args, fn.argtypes))
-        with torch.cuda.device(self.device):
-            probe = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, self.layout,
-                                                     int(xctl is not None))
-        if probe <= 0 or "wave tiles" not in self.describe():
-            return None  # not a wave-tile shape / layout: the host loop
         state = {}
 
         def run():
@@ -521,7 +528,13 @@ class MUPlan:
             else:
                 state["st"] = fn(*cargs)
 
-        def finish():
+        def finish(raise_on_error: bool = True):
+            """(n_iter, errors); with raise_on_error=False a refused launch gives None (the caller
+            agrees the fallback with its peers, as after a failed launch)."""
+            if not raise_on_error and state.get("st", -1) < 0:
+                import warnings
+                warnings.warn(f"cnmf_mu_fit_tol: {self.lib.cnmf_last_error().decode()}", RuntimeWarning)
+                return None
             check(state.get("st", -1), "cnmf_mu_fit_tol")
             out = tolctl.cpu().numpy()
             if out[self._TC["stopped"]] != 0 and out[self._TC["in_snap"]] != 0:
@@ -571,12 +584,13 @@ class MUPlan:
         return self.H64.to(dtype or self.tc)
 
 
-def sync_failed(plan) -> bool:
+def sync_failed(plan, local_failure: bool = False) -> bool:
     """check_sync_error() as a collective verdict: True on EVERY rank of the plan's group when the
     last launch failed on ANY rank (a rank deciding the fallback from its own error word
-    alone re-runs a stretch its peers do not, and the collectives stop matching).  Synchronises."""
+    alone re-runs a stretch its peers do not, and the collectives stop matching).  local_failure:
+    this rank's launch was refused before it ran.  Synchronises."""
     import warnings
-    failed = False
+    failed = bool(local_failure)
     try:
         plan.check_sync_error()
     except _lib.HipLibraryError as e:
@@ -613,12 +627,15 @@ def _iterate_guarded(plan, n_iter: int, update_H: bool):
 def _run_mu_device_tol(plan, max_iter, tol, verbose, return_errors):
     """run_mu's tol > 0 fit as ONE launch with the test on the device; None when not served.  On a
     failed launch (any rank) every rank restores its state and returns None (the host loop runs)."""
-    W0, H0 = plan.W.clone(), plan.H64.clone()
-    with trace_range(f"cnmf:iterations 1..{max_iter} (device tol)"):
-        res = plan.fit_device_tol(max_iter, tol)
-    if res is None:  # not served: nothing was launched
+    prep = plan.prepare_device_tol(max_iter, tol)  # collective: None on every rank or on none
+    if prep is None:  # not served: nothing was launched
         return None
-    if sync_failed(plan):
+    W0, H0 = plan.W.clone(), plan.H64.clone()
+    run, finish = prep
+    with trace_range(f"cnmf:iterations 1..{max_iter} (device tol)"):
+        run()
+        res = finish(raise_on_error=False)
+    if sync_failed(plan, local_failure=res is None):
         plan.W.copy_(W0)
         plan.H64.copy_(H0)
         plan.refresh_basis()
@@ -642,7 +659,7 @@ def run_mu(plan: MUPlan, max_iter: int = 200, tol: float = 1e-4, update_H: bool 
     trajectory [(n_iter, error)] when return_errors).  tol > 0 on a wave-tile persistent plan: ONE
     launch with the tolerance test on the device (MUPlan.fit_device_tol); else stretches of 10
     iterations with the error checked on the host between them."""
-    if tol > 0 and update_H and hasattr(plan, "fit_device_tol") and getattr(plan, "persistent", False):
+    if tol > 0 and update_H and hasattr(plan, "prepare_device_tol") and getattr(plan, "persistent", False):
         res = _run_mu_device_tol(plan, max_iter, tol, verbose, return_errors)
         if res is not None:
             return res if return_errors else res[0]
@@ -725,8 +742,7 @@ class ALSPlan(MUPlan):
 
     def describe(self) -> str:
         if self.persistent:
-            occ2 = os.environ.get("CNMF_ALS_OCC", "2") != "1"
-            return (f"als_iter_wt_kernel<PD={2 if occ2 else 3}, {2 if occ2 else 1} workgroups per CU>: wave "
+            return ("als_iter_wt_kernel<PD=2, 2 workgroups per CU>: wave "
                     "tiles of 16 samples, 4-wave workgroups, in-launch reduction and H-step (one-wave "
                     "block-cyclic-reduction NNLS solves, every workgroup)")
         return "ALS W-step pass + cnmf_reduce_partials + als_basis_kernel per iteration"
@@ -734,8 +750,11 @@ class ALSPlan(MUPlan):
     def tune(self, *args, **kwargs) -> dict:
         return {}  # one layout
 
-    def fit_device_tol(self, *args, **kwargs):
+    def prepare_device_tol(self, *args, **kwargs):
         return None  # the tolerance test of the ALS runs on the host (its loss is not the MU pass's)
+
+    def fit_device_tol(self, *args, **kwargs):
+        return None
 
     def prepare(self, n_iter: int, pass_events=None):
         """As MUPlan.prepare, for the persistent ALS launch."""

@@ -111,14 +111,11 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *   0 = default (4);
  *   4 = wave tiles: one 4-wave workgroup per CU, each wave streaming its own 16-sample (k = 4) or
  *       8-sample (k = 8) tiles with no barrier inside an iteration, W resident in LDS when it fits;
- *   1 = two independent 4-wave workgroups per CU on 64-sample tiles (k = 4);
- *   2 = one 8-wave workgroup per CU whose two halves run in lockstep, half a tile apart (k = 4);
- *   3 = layout 1 with floating tiles: 80 % of the tiles stay with their workgroup (W resident), the
- *       rest is drawn from a pool every iteration (not bit-repeatable: the draw decides the order).
  *   5 = k = 8 only: the wave tiles with both products on the matrix cores (v_mfma_f32_16x16x4_f32,
  *       16-sample tiles; n_rows a multiple of 16, else layout 4);
- * MUPlan.tune() times 4, 1 and 2 (k = 4) or 4 and 5 (k = 8) and keeps the fastest for its plan;
- * other values are CNMF_ERR_ARG. */
+ * MUPlan.tune() times 4 and 5 at k = 8 and keeps the faster for its plan; other values are
+ * CNMF_ERR_ARG.  (Layouts 1-3, the round-1 workgroup-tile kernel, exist in the diagnostic build
+ * only: DESIGN §3.0b.) */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
  * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction
@@ -173,9 +170,11 @@ int cnmf_device_can_access_peer(int device, int peer);
  * idempotent; the current device is restored) — several devices driven from ONE process
  * (cnmf_amd.multidevice) exchange through directly mapped buffers, no IPC. */
 int cnmf_enable_peer_access(int device, int peer);
-/* Workgroups of the persistent launch for this shape and layout (multi: the in-launch exchange
- * form), 0 when the shape runs per-iteration launches; every one is resident for the whole launch
- * (one per CU for the wave tiles), so co-running launches on one device must fit together. */
+/* Workgroups of the persistent launch for this shape and layout, 0 when the shape runs
+ * per-iteration launches; every one is resident for the whole launch (one per CU for the wave
+ * tiles), so co-running launches on one device must fit together.  multi: bit 0 = the in-launch
+ * exchange form (cnmf_mu_iterations_multi), bit 1 = the launch of cnmf_mu_fit_tol (0 when the
+ * device tolerance test does not serve the shape). */
 int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int layout, int multi);
 int cnmf_xbuf_alloc(int world, void** dptr, void* ipc_handle);
 int cnmf_xbuf_open(const void* ipc_handle, void** dptr);

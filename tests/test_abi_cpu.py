@@ -33,6 +33,11 @@ def test_error_paths_return_status():
     # a bad layout is refused before anything touches a device
     assert lib.cnmf_persist_describe(1024, 81, 4, 0, 7, b"\0" * 64, 64) == -1
     assert b"layout" in lib.cnmf_last_error()
+    # the round-1 layouts 1-3 are in the diagnostic build only (VERDICT r3 housekeeping)
+    for v in (1, 2, 3):
+        assert lib.cnmf_persist_describe(1024, 81, 4, 0, v, b"\0" * 64, 64) == -1
+        assert b"diagnostic" in lib.cnmf_last_error()
+    assert lib.cnmf_abi_version() == 301
 
 
 def test_product_library_has_no_diagnostic_switches():

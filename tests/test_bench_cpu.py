@@ -67,7 +67,7 @@ def _worker(rank, world, port, out):
         el, trips = bench.clock_ramp(plan, 0.25, world, torch.device("cpu"), lambda: None)
         ramp_calls = plan.calls
         assert torch.equal(plan.W, W0)  # the ramp restored the state
-        tuned = plan.tune(n_iter=100, rounds=2)
+        tuned = plan.tune(n_iter=100, rounds=2, variants=(4, 1, 2))
         assert torch.equal(plan.W, W0)  # and so did the tuning
         flags = [bench.any_rank(rank == 1, world, torch.device("cpu")),
                  bench.rank0_says(rank == 0, world, torch.device("cpu"))]
@@ -100,3 +100,39 @@ def test_cpu_model_is_named():
 def test_backend_flag_parses(argv, monkeypatch):
     monkeypatch.setattr("sys.argv", ["bench.py"] + argv)
     assert bench.parse().backend == argv[1]
+
+
+def test_launcher_decision():
+    """`--gpus N` never runs fewer ranks than it reports."""
+    d = bench.launcher_decision
+    assert d(1, {}, 0, "nccl") == ("run", None)
+    assert d(8, {}, 8, "nccl") == ("spawn", None)
+    assert d(2, {}, 1, "gloo") == ("spawn", None)  # gloo ranks may share a device
+    assert d(8, {}, 1, "nccl")[0] == "refuse"  # RCCL: one device per rank
+    assert d(2, {"WORLD_SIZE": "2"}, 0, "nccl") == ("run", None)  # the driver's torchrun line
+    assert d(8, {"WORLD_SIZE": "1"}, 8, "nccl")[0] == "refuse"
+    assert d(1, {"WORLD_SIZE": "4"}, 8, "nccl")[0] == "refuse"
+
+
+def _bench_cmd(extra, env):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in dict(os.environ, **env).items() if v is not None}
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--no-cpu"] + extra, env=env,
+                          cwd=root, capture_output=True, text=True, timeout=240)
+
+
+@pytest.mark.timeout(300)
+def test_gpus_flag_without_launcher_never_reports_one_rank():
+    """`bench.py --gpus 2` without torchrun starts two ranks itself (here, without a GPU, they fail
+    — the point is that no line claiming n_gpus 1 is printed and the exit status is non-zero);
+    a WORLD_SIZE that disagrees with --gpus is refused before anything runs."""
+    r = _bench_cmd(["--gpus", "2", "--backend", "gloo", "--steps", "1", "--warmup", "1"],
+                   {"WORLD_SIZE": None, "RANK": None, "LOCAL_RANK": None})
+    assert "starting 2 ranks" in r.stderr, r.stderr[-2000:]
+    assert '"n_gpus": 1' not in r.stdout
+    if not torch.cuda.is_available():
+        assert r.returncode != 0
+    r = _bench_cmd(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "refused" in r.stderr and '"n_gpus"' not in r.stdout

@@ -244,7 +244,7 @@ class _FlakyExchangePlan(_NumpyPlan):
             self._fail_next, self._err = False, True
             self.Wn = self.Wn * 2.0  # the failed launch's results are invalid
 
-    def fit_device_tol(self, *a, **kw):
+    def prepare_device_tol(self, *a, **kw):
         return None  # the host-checked stretches (the path this test exercises)
 
     def check_sync_error(self):

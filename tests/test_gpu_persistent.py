@@ -1,4 +1,4 @@
-"""GPU parity of the persistent multi-iteration launch (mu_iter_sl_kernel: fp32, F = 81, k = 4).
+"""GPU parity of the persistent multi-iteration launch (mu_iter_wt_kernel: fp32, F = 81, k = 4).
 
 The persistent kernel runs the sample pass, the cross-workgroup reduction and the basis update of
 every iteration inside ONE launch.  It must give the fp64 oracle's factors within the north_star
@@ -36,12 +36,10 @@ def _unfused(plan, n):
         plan.basis_update()
 
 
-@pytest.fixture(params=[4, 1, 2, 3], ids=["wave", "pairs", "teams", "floating"])
+@pytest.fixture(params=[4], ids=["wave"])
 def layout(request):
-    """The persistent launch's layouts (the plan's `layout` argument): wave tiles, pairs of 4-wave
-    workgroups per CU, one 8-wave two-team workgroup per CU (lockstep halves, half a tile apart), or
-    pairs with floating tiles (a pool drawn every iteration; shapes with < 4 static tiles per
-    workgroup fall back to pairs)."""
+    """The persistent launch's layouts in the product library (the plan's `layout` argument): the
+    wave tiles.  (The round-1 layouts 1-3 are in the diagnostic build only since round 4.)"""
     return request.param
 
 
@@ -70,27 +68,23 @@ def test_persistent_matches_oracle(n_tiles, layout):
     assert plan.counters_at_rest()  # counters back at rest
 
 
-def test_layouts_agree_and_are_deterministic():
-    """The two layouts group the per-workgroup fp32 partial sums differently: agreement to fp32
-    summation-order noise; each is bit-for-bit repeatable, also across split launches."""
+def test_wave_tiles_are_deterministic_and_the_only_product_layout():
+    """Bit-for-bit repeatable, also across split launches; layouts 1-3 are refused by the product."""
     import torch
+    from cnmf_amd import _lib
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(64 * 3001, 81, seed=21, dtype=np.float32)
     W0, H0 = random_init(X, 4, 5)
-    out = {}
-    for v in (4, 1, 2):
-        a, c = _plan(X, W0, H0, v), _plan(X, W0, H0, v)
-        a.iterate(60)
-        for n in (7, 23, 30):
-            c.iterate(n)
-        a.check_sync_error()
-        c.check_sync_error()
-        assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
-        out[v] = (a.W.cpu().numpy(), a.H64.cpu().numpy())
-    # a plan's layout is its own: two plans with different layouts side by side
-    assert "wt_kernel" in _plan(X, W0, H0, 4).describe() and "sl_kernel" in _plan(X, W0, H0, 1).describe()
-    for v in (2, 4):
-        assert rel_fro(out[1][0], out[v][0]) < 1e-6 and rel_fro(out[1][1], out[v][1]) < 1e-6
+    a, c = _plan(X, W0, H0, 4), _plan(X, W0, H0, 4)
+    a.iterate(60)
+    for n in (7, 23, 30):
+        c.iterate(n)
+    a.check_sync_error()
+    c.check_sync_error()
+    assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
+    assert "wt_kernel" in a.describe()
+    with pytest.raises(_lib.HipLibraryError, match="diagnostic"):
+        _plan(X, W0, H0, 1).iterate(1)
 
 
 def test_persistent_agrees_with_per_iteration_launches():
@@ -138,36 +132,6 @@ def test_persistent_tol_stop_through_api():
                                max_iter=400, tol=1e-4)
     assert n == nr
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32
-
-
-# the product's resident fraction is 0.8 (CNMF_DYN_FRAC varies it in the diagnostic build only):
-# cfg2's tile count, a count with the minimum static tiles, a ragged count
-@pytest.mark.parametrize("n_tiles", [4096, 15625, 3001])
-def test_floating_tiles(n_tiles):
-    """Layout 3: tiles drawn from a pool every iteration, their W handed between workgroups (and
-    XCDs) through HBM.  Every tile must be updated exactly once per iteration: the factors match the
-    oracle and the static layout (to fp32 summation-order noise), across split launches too, and the
-    counters (tickets and both pools) are back at rest."""
-    from cnmf_amd.synthetic import iop_spectra, random_init
-    X = iop_spectra(64 * n_tiles, 81, seed=n_tiles + 3, dtype=np.float32)
-    W0, H0 = random_init(X, 4, 11)
-    n_it = 60 if n_tiles < 15625 else 30
-    ref = _plan(X, W0, H0, 1)
-    ref.iterate(n_it)
-    a, c = _plan(X, W0, H0, 3), _plan(X, W0, H0, 3)
-    a.iterate(n_it)
-    for n in (2, n_it // 2 - 2, n_it - n_it // 2):
-        c.iterate(n)
-    for p in (a, c):
-        p.check_sync_error()
-        assert p.counters_at_rest()
-    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
-                              max_iter=n_it, tol=0.0)
-    for p in (a, c):
-        W, H = p.W.cpu().numpy(), p.H64.cpu().numpy()
-        assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
-        assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6 and rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
-
 
 
 def test_failed_persistent_launch_falls_back():

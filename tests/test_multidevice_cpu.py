@@ -56,3 +56,42 @@ def test_devices_argument_validation():
     from cnmf_amd.multidevice import MultiDeviceFit
     with pytest.raises(ValueError):
         MultiDeviceFit(torch.zeros(4, 3), None, 2, (0, 0, 0, 0), [])
+
+
+def test_host_all_reduce_works_after_a_failed_exchange_setup(monkeypatch):
+    """a failed enable_exchange aborts the group's barrier; the fallback (the host
+    all-reduce of the same group) must still work afterwards instead of raising BrokenBarrierError."""
+    import contextlib
+    import types
+
+    from cnmf_amd import _lib
+    from cnmf_amd import multidevice as md
+
+    class _Plan:
+        def __init__(self, r):
+            self.device, self.exchange, self.r = torch.device("cpu"), False, r
+
+        def enable_exchange(self):
+            if self.r == 1:  # one shard cannot map its peers; the others would wait in a rendezvous
+                raise _lib.HipLibraryError("in-launch exchange unavailable: no peer access")
+            fit.group.view(self.r).all_gather(self.r)
+
+    fit = object.__new__(md.MultiDeviceFit)
+    fit.plans = [_Plan(r) for r in range(3)]
+    fit.group = LocalGroup(3)
+    fit.streams = [None] * 3
+    fit.shared_device_exchange, fit.exchange = False, False
+    monkeypatch.setattr(md.torch.cuda, "set_device", lambda d: None)
+    monkeypatch.setattr(md.torch.cuda, "stream", lambda s: contextlib.nullcontext())
+    monkeypatch.setattr(md.torch.cuda, "current_stream", lambda: types.SimpleNamespace(synchronize=lambda: None))
+    monkeypatch.setattr(md, "_exchange_fits", lambda plans, shared=False: True)
+    with pytest.warns(RuntimeWarning):
+        assert fit.enable_exchange() is False
+    out = [None] * 3
+
+    def go(r, plan):
+        t = torch.tensor([float(r + 1)], dtype=torch.float64)
+        fit.group.view(r).all_reduce(t, "sum")
+        out[r] = float(t[0])
+    fit._run(go)
+    assert out == [6.0, 6.0, 6.0]

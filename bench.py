@@ -3,18 +3,19 @@ GB/s vs peak, V = 1e6 x 81, k = 4, at 1/2/4/8 GPUs; configs[1] = cfg2 at one GPU
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
-    python bench.py --rows 10000000 --k 8             # cfg3 (its 8-GPU run: --gpus 8 via torchrun)
-    python bench.py --scaling weak                    # every GPU owns 1e6 rows (aggregate line)
+    python bench.py --rows 10000000 --k 8             # cfg3's rows on one GPU
+    python bench.py --rows 10000000 --k 8 --scaling strong   # cfg3 as one 1e7-row problem over the GPUs
     python bench.py --solver als                      # cfg5, the constrained ALS
     python bench.py --features 300 --k 16 --dtype bf16   # cfg4, the bf16 matrix-core pass
 
 One "step" = one MU iteration (sample pass over X + cross-workgroup reduction + basis update) on
 synthetic IOP spectra (cnmf_amd.synthetic), fp32, tol = 0, inputs resident in HBM before the timed
-region.  Default --scaling strong: V = --rows x 81 (1e6 x 81) is ONE problem whose rows are split
-over the N ranks in 64-row-aligned shards; the k(F+k) fp64 accumulators are all-reduced once per
-iteration (inside the persistent launch over xGMI when validated, else RCCL); value = iterations
-per second of that problem (exactly cfg2's it/s at N = 1).  --scaling weak: every rank owns --rows
-rows, value = sum over ranks of (rows / 1e6) x iterations / s.
+region.  Default --scaling weak (the task's rule for a path that shards its units: every rank owns
+--rows = 1e6 rows of the sample axis, and the k(F+k) fp64 accumulators — the path's one exchange —
+are all-reduced every iteration, inside the persistent launch over xGMI when validated, else RCCL):
+value = the 1e6-row MU iterations all ranks completed per second (N x rows / 1e6 x K / time;
+exactly cfg2's it/s at N = 1).  --scaling strong: V = --rows x 81 is ONE problem whose rows are
+split over the N ranks in 64-row-aligned shards, value = iterations per second of that problem.
 
 Extra keys: roofline (the dominant kernel timed with HIP events on its launch stream inside the
 timed region: at N = 1 the ONE persistent launch that runs all K iterations, else each per-iteration
@@ -48,10 +49,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=1000)
     p.add_argument("--rows", type=int, default=1_000_000,
                    help="rows of V: the whole problem (--scaling strong) or per GPU (--scaling weak)")
-    p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                   help="strong (default): the BASELINE metric's fixed V (1e6 x 81) split over the "
-                        "GPUs, value = iterations/s of that problem; weak: every GPU owns --rows "
-                        "rows, value = iterations/s of a 1e6-row problem summed over GPUs")
+    p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                   help="weak (default): every GPU owns --rows rows (V = 1e6 x 81 per GPU), value = "
+                        "1e6-row iterations/s summed over the GPUs; strong: --rows is ONE problem split "
+                        "over the GPUs, value = iterations/s of that problem")
     p.add_argument("--features", type=int, default=81)
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
@@ -400,7 +401,7 @@ def main():
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     exchange = None
-    if dist_path and args.exchange == "auto" and plan.persistent_shape:
+    if dist_path and args.exchange == "auto" and plan.exchange_shape:
         exchange = validate_exchange(plan, W0, H0d)
         print(f"[rank {rank}] in-launch exchange: {exchange}", file=sys.stderr, flush=True)
     elif args.dist and args.solver == "mu" and not args.weighted:
@@ -547,8 +548,7 @@ def main():
     elif args.solver == "als":
         kname = "constrained-ALS W-step pass (mu_pass_kernel<..., ALS>: exact FCLS per sample + [WᵀX|WᵀW])"
     elif persistent:
-        kbase = next((kn for kn in ("mu_iter_mf8_kernel", "mu_iter_wt_kernel") if kn in (layout or "")),
-                     "mu_iter_sl_kernel")
+        kbase = (layout or "").split("<")[0].split(":")[0].strip() or "persistent kernel"
         if world == 1:
             kname = (f"{kbase} (persistent: K iterations of pass + in-launch reduction + basis "
                      "update per launch)")
@@ -559,7 +559,8 @@ def main():
         kname = ("mu_iter_sl_kernel shard step (one iteration per launch: pending basis update, "
                  "pass, in-launch reduction; all_reduce between launches)")
     else:
-        kname = "sample pass (mu_pass_kernel / mu_pass_mfma_kernel)"
+        kname = ("iteration as launches (sample pass + reduction + basis update; events around the whole "
+                 "iteration)")
     roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": traffic_src,
@@ -604,10 +605,13 @@ def main():
                         f"{args.dtype} synthetic IOP spectra, rows split over {world} GPU(s) in "
                         f"64-row-aligned shards (strong scaling: the problem is fixed)")
         else:
-            metric = "MU iterations/sec (V=1e6x81 k=4 synthetic IOP per GPU) & achieved HBM GB/s vs peak"
+            metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6\u00d781 k=4, 1/2/4/8 GPU"
+                      if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
             workload = (f"{cfg}: MU (Frobenius, tol={args.tol:g}) on V={n_rows}x{F} per GPU, k={k}, "
-                        f"{args.dtype} synthetic IOP spectra (weak scaling: every GPU owns this "
-                        f"many rows)")
+                        f"{args.dtype} synthetic IOP spectra (weak scaling: every GPU owns its own "
+                        f"{n_rows} rows of one {world * n_rows}-row problem, [WᵀX | WᵀW] all-reduced "
+                        f"every iteration; value = {n_rows / 1e6:g}e6-row iterations/s summed over "
+                        f"the {world} GPU(s))")
     out = {
         "metric": metric,
         "value": round(value, 2),

@@ -253,10 +253,26 @@ __device__ unsigned long long g_stamps[16];
       for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamps[i_], st_acc[i_]);           \
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_stamps[8], 1ull);                       \
   } while (0)
+// the end of a persistent bfw iteration: thread 0 of every workgroup sums the phase durations
+// (s_memtime) into g_eoi[slot]; g_eoi[15] counts the (workgroup, iteration) pairs
+__device__ unsigned long long g_eoi[16];
+#define EOI_DECL unsigned long long eoi_t0 = 0;
+#define EOI(slot)                                                                     \
+  do {                                                                                \
+    if (threadIdx.x == 0) {                                                           \
+      unsigned long long st_t;                                                        \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_t) :: "memory");  \
+      if (slot > 0) atomicAdd(&g_eoi[slot], st_t - eoi_t0);                           \
+      else atomicAdd(&g_eoi[15], 1ull);                                               \
+      eoi_t0 = st_t;                                                                  \
+    }                                                                                 \
+  } while (0)
 #else
 #define STAMP_DECL
 #define STAMP(slot) do {} while (0)
 #define STAMP_FLUSH do {} while (0)
+#define EOI_DECL
+#define EOI(slot) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -1152,7 +1168,7 @@ __host__ __device__ inline Lds lds(int F) {
   L.xbytes = (int)align16((size_t)TSW * L.xrow + 64);  // + 64 zero bytes for the reads past the last row
   L.slotb = L.xbytes + TSW * 16 * 4;                   // + the wave tile's W [16][k <= 16] fp32
   L.slot = (int)align16((size_t)L.hht + 16 * 16 * 8);
-  L.red = 2 * (NBX + 1) * 4 * 64 * 8;                  // end of launch: two waves' fp64 sums
+  L.red = 4 * ((NBX + 2) / 2) * 4 * 64 * 8;            // end of an iteration: four waves' fp64 sums, half the blocks
   const int loop = L.slot + 8 * L.slotb;  // two wave-tile slots per wave
   L.total = loop > L.red ? loop : L.red;
   return L;
@@ -1190,267 +1206,6 @@ __device__ __forceinline__ void stage_x(unsigned base, const u32x4* pf, int l, i
 }
 }  // namespace bw
 
-// KSC > 0: K-steps (and 2·KSC feature blocks) and KC components at compile time (cfg4: KSC = 10,
-// F in 289..320, KC = 16): fully unrolled, branch-free phases the scheduler can interleave (with
-// runtime bounds every K-step and feature block was its own basic block: phases 1 and 3 ran as
-// dependent chains, 2647 and 2263 cycles per wave tile, profiles/r03/bfw/); KSC = 0: runtime F, k.
-template <int KSC, int KC>
-__global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __restrict__ X, float* __restrict__ W,
-                                                            const double* __restrict__ Ht,
-                                                            const double* __restrict__ HHt,
-                                                            double* __restrict__ partials, int64_t n_rows, int F,
-                                                            int k, double l1, double l2, int flags,
-                                                            int64_t n_tiles) {
-  using namespace bw;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Lds L = lds(F);
-  const int t = threadIdx.x;
-  const int l = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int g = l >> 4, li = l & 15;
-  const int KS = KSC ? KSC : bm::ksteps(F);
-  const int NB = KSC ? 2 * KSC : (F + 15) / 16;  // KSC: the last blocks past F read finite pads / rows
-  if (KC) k = KC;
-  const int nchx = 2 * F, nchw = 4 * k;  // 16-byte chunks of a wave tile's X and W
-  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
-  // this wave's two slots (a pair of wave tiles per body): X tile [16][F] bf16 (+ zero pad), W [16][k]
-  unsigned char* xsp[2] = {smem + L.slot + (2 * w) * L.slotb, smem + L.slot + (2 * w + 1) * L.slotb};
-  const int XR = L.xrow;
-  const unsigned xpad = (unsigned)(XR - 2 * F), mrow = (unsigned)((0x100000000ull + 2 * F - 1) / (2 * F));
-
-  // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
-  for (int e = t; e < bm::KP * 32 * KS; e += NT) {
-    const int n = e / (32 * KS);
-    const int f = e - n * 32 * KS;
-    const double h = (n < k && f < F) ? Ht[(size_t)f * bm::KP + n] : 0.0;
-    const uint16_t h1 = bm::bf16_rn((float)h);
-    const double r1 = h - (double)bm::bf16_f(h1);
-    const uint16_t h2 = bm::bf16_rn((float)r1);
-    const double r2 = r1 - (double)bm::bf16_f(h2);
-    const uint16_t h3 = bm::bf16_rn((float)r2);
-    uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;
-    row[0] = h1;
-    row[bm::KP * L.hrow / 2] = h2;
-    row[2 * bm::KP * L.hrow / 2] = h3;
-  }
-  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
-  for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = HHt[e];
-  if (l < 16) {  // the slots' zero pads: past the last row, and (never staged) each row's tail
-    reinterpret_cast<uint32_t*>(xsp[0] + TSW * XR)[l] = 0u;
-    reinterpret_cast<uint32_t*>(xsp[1] + TSW * XR)[l] = 0u;
-  }
-  for (int e = l; e < TSW * (int)(xpad / 4); e += 64) {
-    const int r = e / (int)(xpad / 4), c = e - r * (int)(xpad / 4);
-    reinterpret_cast<uint32_t*>(xsp[0] + r * XR + 2 * F)[c] = 0u;
-    reinterpret_cast<uint32_t*>(xsp[1] + r * XR + 2 * F)[c] = 0u;
-  }
-  __syncthreads();
-  double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li]
-#pragma unroll
-  for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * bm::KP + li];
-
-  // ---- this wave's tiles: rows [64·(blockIdx + G·i) + 16w, +16), i < ntw (full 64-sample tiles)
-  const int64_t G = gridDim.x;
-  const int ntw = (int)((n_tiles - blockIdx.x + G - 1) / G);
-  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(X);
-  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(W);
-  auto row0 = [&](int i) -> int64_t {  // first row of wave tile i (past the last: row 16w of tile 0)
-    return 64 * (i < ntw ? (int64_t)blockIdx.x + G * i : (int64_t)blockIdx.x) + 16 * w;
-  };
-  auto prefetch = [&](u32x4 (&pf)[PFS], int i) {
-    const int64_t r0 = row0(i);
-    const unsigned char* xsrc = Xb + (size_t)r0 * F * 2;
-#pragma unroll
-    for (int u = 0; u < PFX; ++u) ld16(pf[u], xsrc + 16 * (l + 64 * u < nchx ? l + 64 * u : l));
-    ld16(pf[PFX], Wb + (size_t)r0 * k * 4 + 16 * (l < nchw ? l : 0));
-  };
-  auto stage = [&](const u32x4 (&pf)[PFS], unsigned char* xs) {
-    stage_x<0>((unsigned)(uintptr_t)xs, pf, l, nchx, mrow, xpad);
-    // W [16][k]: at k = 16 the lane's chunk (s = l/4, j = l%4) goes to chunk j ^ ((s >> 1) & 3) of row s,
-    // so phase 2's column reads (16 samples × 2 components per half-wave) spread over 16 banks, not 4
-    const int wch = KC == 16 ? (l & ~3) | ((l & 3) ^ ((l >> 3) & 3)) : l;
-    if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * wch), pf[PFX]);
-  };
-
-  // accumulators: phase 3's fp32 MFMA chains over the wave's tiles (in AGPRs: no VALU touches
-  // them before the end of the launch, so the 20 block chains run interleaved)
-  f32x4 cacc[NBX], bacc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int nb = 0; nb < NBX; ++nb) cacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // invalid lanes' stores land in this workgroup's partial row (rewritten at the end of the launch;
-  // the host guarantees k(F+k) >= 1024 doubles): every wave tile issues exactly NSTB stores per lane
-  float* dummy = reinterpret_cast<float*>(partials + (size_t)blockIdx.x * k * (F + k)) + 64 * w + l;
-  STAMP_DECL
-
-  // phase 1 for a PAIR of wave tiles: each K-step's three H terms are read from LDS once for both
-  // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body)
-  auto phase1 = [&](double (&n0)[4], double (&n1)[4]) {
-    const unsigned char* xa0 = xsp[0] + li * XR + 16 * g;
-    const unsigned char* xa1 = xsp[1] + li * XR + 16 * g;
-    const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
-#pragma unroll
-    for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
-      if (!KSC && ks >= KS) break;
-      const s16x8 a = *reinterpret_cast<const s16x8*>(xa0 + 64 * ks);  // 16-B aligned rows: one b128
-      const s16x8 c = *reinterpret_cast<const s16x8*>(xa1 + 64 * ks);
-      const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
-      const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
-      const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
-      const bf16x8 av = __builtin_bit_cast(bf16x8, a), cv = __builtin_bit_cast(bf16x8, c);
-      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f}, v = f32x4{0.f, 0.f, 0.f, 0.f};
-      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
-      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
-      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b2, u, 0, 0, 0);
-      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b2, v, 0, 0, 0);
-      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, u, 0, 0, 0);
-      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b1, v, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        n0[r] += (double)u[r];
-        n1[r] += (double)v[r];
-      }
-    }
-  };
-  // phases 2 and 3 of one wave tile (slot p, first row r0; invalid: w' = 0 and dummy stores)
-  auto update = [&](int p, int64_t r0, bool valid, const double (&num64)[4]) {
-    const unsigned char* xs = xsp[p];
-    const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);
-    auto wix = [&](int s, int m) { return KC == 16 ? 16 * s + (m ^ (((s >> 1) & 3) << 2)) : s * k + m; };
-    // phase 2: den = w·HHᵀ (f64 MFMA; A row ρ = li carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is
-    // sample 4g + r), then w' = w·num/den (SK:553-629) for (s = 4g + r, n = li)
-    f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
-    const int sa = 4 * (li & 3) + (li >> 2);
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int m = 4 * kk + g;
-      const double av = m < k ? (double)wso[wix(sa, m)] : 0.0;
-      den = __builtin_amdgcn_mfma_f64_16x16x4f64(av, hhb[kk], den, 0, 0, 0);
-    }
-    float wr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int s = 4 * g + r;
-      float wn = 0.f;
-      if (li < k) {
-        double d = den[r];
-        const double wold = (double)wso[wix(s, li)];
-        if (l1 > 0.0) d += l1;              // SK:616-617
-        if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
-        if (d == 0.0) d = EPS32;            // SK:620
-        wn = (float)(wold * (num64[r] / d));  // SK:622-629
-      }
-      wn = valid ? wn : 0.f;
-      wr[r] = wn;
-      float* dst = (valid && li < k) ? W + (size_t)(r0 + s) * k + li : dummy + 256 * (r + 4 * p);
-      *dst = wn;
-    }
-    if (!do_acc) return;
-    // phase 3: A[m = 4g + r][f = 16nb + li] and B[m][n] over the tile's 16 samples
-    s16x4 a1, a2, a3;  // w'[4g + j][li] in three bf16 terms: the A operand (row m = li, k = 4g + j)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint16_t h1 = bm::bf16_rn(wr[j]);
-      const float r1 = wr[j] - bm::bf16_f(h1);
-      const uint16_t h2 = bm::bf16_rn(r1);
-      const float r2 = r1 - bm::bf16_f(h2);
-      a1[j] = (short)h1;
-      a2[j] = (short)h2;
-      a3[j] = (short)bm::bf16_rn(r2);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
-    const int q = li >> 2, pp = li & 3;
-    const unsigned char* xb0 = xs + (4 * g + q) * XR + 8 * pp;
-#pragma unroll
-    for (int nb = 0; nb < NBX; ++nb) {
-      if (nb < (KSC ? 2 * KSC : NB)) {
-        const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb0 + 32 * nb));
-        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a3, b, cacc[nb], 0, 0, 0);
-        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, b, cacc[nb], 0, 0, 0);
-        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, b, cacc[nb], 0, 0, 0);
-      }
-    }
-  };
-
-  u32x4 pf[PD][PFS];
-  static_assert(PD == 2, "a pair of wave tiles per body");
-  prefetch(pf[0], 0);
-  prefetch(pf[1], 1);
-#pragma unroll
-  for (int d = 0; d < 2 * NSTB; ++d)  // as if a body had run: the first waits count exactly
-    asm volatile("global_store_dword %0, %1, off" ::"v"(dummy + 256 * d), "v"(0) : "memory");
-  for (int i0 = 0; i0 < ntw; i0 += 2) {
-    STAMP(0);
-    // younger than set 0: set 1's loads and the previous body's 2·NSTB stores; than set 1: the stores
-    wait_set<PFS + 2 * NSTB>(pf[0]);
-    stage(pf[0], xsp[0]);
-    wait_set<2 * NSTB>(pf[1]);
-    stage(pf[1], xsp[1]);
-    STAMP(1);  // 1: waits + staging
-    prefetch(pf[0], i0 + 2);
-    prefetch(pf[1], i0 + 3);
-    STAMP(2);  // 2: prefetch issue
-    double n0[4] = {0.0, 0.0, 0.0, 0.0}, n1[4] = {0.0, 0.0, 0.0, 0.0};
-    phase1(n0, n1);
-    STAMP(3);  // 3: phase 1 (both tiles)
-    update(0, row0(i0), true, n0);
-    STAMP(4);  // 4: phases 2 + 3 of the first tile
-    update(1, row0(i0 + 1), i0 + 1 < ntw, n1);
-    STAMP(5);  // 5: phases 2 + 3 of the second tile
-  }
-  STAMP_FLUSH;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup
-  if (!do_acc) return;
-
-  // ---- the workgroup's partial row [k][F + k]: the waves' sums in the order (w0 + w2) + (w1 + w3)
-  __syncthreads();  // every wave done with its slot: LDS is reused from offset 0
-  double* red = reinterpret_cast<double*>(smem);  // [2][NBX + 1][4][64]
-  auto put = [&](int slot) {
-#pragma unroll
-    for (int nb = 0; nb < NBX; ++nb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[((slot * (NBX + 1) + nb) * 4 + r) * 64 + l] = (double)cacc[nb][r];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) red[((slot * (NBX + 1) + NBX) * 4 + r) * 64 + l] = (double)bacc[r];
-  };
-  double sa64[NBX + 1][4];
-#pragma unroll
-  for (int nb = 0; nb < NBX; ++nb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) sa64[nb][r] = (double)cacc[nb][r];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) sa64[NBX][r] = (double)bacc[r];
-  if (w >= 2) put(w - 2);
-  __syncthreads();
-  if (w < 2)
-#pragma unroll
-    for (int nb = 0; nb <= NBX; ++nb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) sa64[nb][r] += red[((w * (NBX + 1) + nb) * 4 + r) * 64 + l];
-  __syncthreads();
-  if (w == 1)
-#pragma unroll
-    for (int nb = 0; nb <= NBX; ++nb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(nb * 4 + r) * 64 + l] = sa64[nb][r];
-  __syncthreads();
-  if (w != 0) return;
-  const int V = F + k;
-  double* prow = partials + (size_t)blockIdx.x * k * V;
-#pragma unroll
-  for (int nb = 0; nb <= NBX; ++nb)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double v = sa64[nb][r] + red[(nb * 4 + r) * 64 + l];
-      const int m = 4 * g + r;
-      if (nb < NBX) {
-        const int f = 16 * nb + li;
-        if (m < k && f < F) prow[(size_t)m * V + f] = v;
-      } else if (m < k && li < k) {
-        prow[(size_t)m * V + F + li] = v;
-      }
-    }
-}
 
 // ------------------------------------------------------------------------------------------------
 // The sample-lane pass: the IOP grid's headline shape (F = 81, k = 4, fp32 X and W), full tiles.
@@ -2506,6 +2261,530 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// The arguments of the bf16 wave-tile pass and of its persistent form (mu_iter_bfw_kernel).
+struct BfwArgs {
+  const bf16_t* X;
+  float* W;
+  const double* Ht;   // the pass: the basis (Hᵀ fp64 [F][16], HHᵀ [16][16])
+  const double* HHt;
+  double* partials;   // [G][k(F+k)]
+  int64_t n_rows;
+  int F, k;
+  double l1, l2;
+  int flags;
+  int64_t n_tiles;    // full 64-sample tiles
+  // PERSIST (mu_iter_bfw_kernel): n_iter MU iterations in ONE launch
+  double* H64;        // in: the basis [k][F]; out: the final basis
+  double* Ht_out;     // out: Hᵀ [F][16], HHᵀ [16][16] of the final basis
+  double* HHt_out;
+  double* AB;         // out: the last iteration's [WᵀX | WᵀW] (k(F+k))
+  uint32_t* cnt;      // counters (at rest on entry, left at rest): CNT_GROUP0 / CNT_TOP = the two
+                      // grid barriers of an iteration, CNT_ERR
+  int n_iter;
+  double l1H, l2H;
+};
+
+// KSC > 0: K-steps (and 2·KSC feature blocks) and KC components at compile time (cfg4: KSC = 10,
+// F in 289..320, KC = 16): fully unrolled, branch-free phases the scheduler can interleave (with
+// runtime bounds every K-step and feature block was its own basic block: phases 1 and 3 ran as
+// dependent chains, 2647 and 2263 cycles per wave tile, profiles/r03/bfw/); KSC = 0: runtime F, k.
+// PERSIST (KSC = 10, KC = 16 only): the n_iter iterations of mu_iter_bfw_kernel (below).
+template <int KSC, int KC, bool PERSIST>
+__device__ __forceinline__ void bfw_run(const BfwArgs& a) {
+  using namespace bw;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const bf16_t* __restrict__ X = a.X;
+  float* __restrict__ W = a.W;
+  double* __restrict__ partials = a.partials;
+  int F = a.F, k = a.k;
+  const double l1 = a.l1, l2 = a.l2;
+  const int flags = PERSIST ? (CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE) : a.flags;
+  const int64_t n_tiles = a.n_tiles;
+  const Lds L = lds(F);
+  const int t = threadIdx.x;
+  const int l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int g = l >> 4, li = l & 15;
+  const int KS = KSC ? KSC : bm::ksteps(F);
+  const int NB = KSC ? 2 * KSC : (F + 15) / 16;  // KSC: the last blocks past F read finite pads / rows
+  if (KC) k = KC;
+  const int nchx = 2 * F, nchw = 4 * k;  // 16-byte chunks of a wave tile's X and W
+  const bool do_acc = (flags & CNMF_PASS_ACCUMULATE) != 0;
+  // this wave's two slots (a pair of wave tiles per body): X tile [16][F] bf16 (+ zero pad), W [16][k]
+  unsigned char* xsp[2] = {smem + L.slot + (2 * w) * L.slotb, smem + L.slot + (2 * w + 1) * L.slotb};
+  const int XR = L.xrow;
+  const unsigned xpad = (unsigned)(XR - 2 * F), mrow = (unsigned)((0x100000000ull + 2 * F - 1) / (2 * F));
+
+  // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
+  double* sHHt = reinterpret_cast<double*>(smem + L.hht);
+  double* sH64 = reinterpret_cast<double*>(smem + L.total);  // PERSIST: the fp64 basis [k][F]
+  auto put_terms = [&](auto hval) {
+    for (int e = t; e < bm::KP * 32 * KS; e += NT) {
+      const int n = e / (32 * KS);
+      const int f = e - n * 32 * KS;
+      const double h = (n < k && f < F) ? hval(n, f) : 0.0;
+      const uint16_t h1 = bm::bf16_rn((float)h);
+      const double r1 = h - (double)bm::bf16_f(h1);
+      const uint16_t h2 = bm::bf16_rn((float)r1);
+      const double r2 = r1 - (double)bm::bf16_f(h2);
+      const uint16_t h3 = bm::bf16_rn((float)r2);
+      uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;
+      row[0] = h1;
+      row[bm::KP * L.hrow / 2] = h2;
+      row[2 * bm::KP * L.hrow / 2] = h3;
+    }
+  };
+  // PERSIST: the terms and HHᵀ from the fp64 basis in LDS (thread = entry (j, m) of HHᵀ: four
+  // interleaved chains over f combined in a fixed order — every workgroup the same bits, and HHᵀ
+  // exactly symmetric)
+  auto derive = [&]() {
+    put_terms([&](int n, int f) { return sH64[n * F + f]; });
+    const int j = t >> 4, m = t & 15;
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+    if (j < k && m < k) {
+      const double* hj = sH64 + j * F;
+      const double* hm = sH64 + m * F;
+      int f = 0;
+      for (; f + 4 <= F; f += 4) {
+        c0 = fma(hj[f], hm[f], c0);
+        c1 = fma(hj[f + 1], hm[f + 1], c1);
+        c2 = fma(hj[f + 2], hm[f + 2], c2);
+        c3 = fma(hj[f + 3], hm[f + 3], c3);
+      }
+      for (; f < F; ++f) c0 = fma(hj[f], hm[f], c0);
+    }
+    static_assert(NT == bm::KP * bm::KP, "one thread per HHᵀ entry");
+    sHHt[t] = (c0 + c1) + (c2 + c3);
+  };
+  // the slots' zero pads: past the last row, and (never staged) each row's tail
+  auto zero_pads = [&]() {
+    if (l < 16) {
+      reinterpret_cast<uint32_t*>(xsp[0] + TSW * XR)[l] = 0u;
+      reinterpret_cast<uint32_t*>(xsp[1] + TSW * XR)[l] = 0u;
+    }
+    for (int e = l; e < TSW * (int)(xpad / 4); e += 64) {
+      const int r = e / (int)(xpad / 4), c = e - r * (int)(xpad / 4);
+      reinterpret_cast<uint32_t*>(xsp[0] + r * XR + 2 * F)[c] = 0u;
+      reinterpret_cast<uint32_t*>(xsp[1] + r * XR + 2 * F)[c] = 0u;
+    }
+  };
+  if constexpr (PERSIST) {
+    for (int e = t; e < k * F; e += NT) sH64[e] = a.H64[e];
+    __syncthreads();
+    derive();
+  } else {
+    put_terms([&](int n, int f) { return a.Ht[(size_t)f * bm::KP + n]; });
+    for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = a.HHt[e];
+  }
+  zero_pads();
+  __syncthreads();
+  double hhb[4];  // B operand of the den MFMA: HHᵀ[m = 4kk + g][n = li]
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * bm::KP + li];
+
+  // ---- this wave's tiles: rows [64·(blockIdx + G·i) + 16w, +16), i < ntw (full 64-sample tiles)
+  const int64_t G = gridDim.x;
+  const int ntw = (int)((n_tiles - blockIdx.x + G - 1) / G);
+  const unsigned char* Xb = reinterpret_cast<const unsigned char*>(X);
+  const unsigned char* Wb = reinterpret_cast<const unsigned char*>(W);
+  auto row0 = [&](int i) -> int64_t {  // first row of wave tile i (past the last: row 16w of tile 0)
+    return 64 * (i < ntw ? (int64_t)blockIdx.x + G * i : (int64_t)blockIdx.x) + 16 * w;
+  };
+  auto prefetch = [&](u32x4 (&pf)[PFS], int i) {
+    const int64_t r0 = row0(i);
+    const unsigned char* xsrc = Xb + (size_t)r0 * F * 2;
+#pragma unroll
+    for (int u = 0; u < PFX; ++u) ld16(pf[u], xsrc + 16 * (l + 64 * u < nchx ? l + 64 * u : l));
+    ld16(pf[PFX], Wb + (size_t)r0 * k * 4 + 16 * (l < nchw ? l : 0));
+  };
+  auto stage = [&](const u32x4 (&pf)[PFS], unsigned char* xs) {
+    stage_x<0>((unsigned)(uintptr_t)xs, pf, l, nchx, mrow, xpad);
+    // W [16][k]: at k = 16 the lane's chunk (s = l/4, j = l%4) goes to chunk j ^ ((s >> 1) & 3) of row s,
+    // so phase 2's column reads (16 samples × 2 components per half-wave) spread over 16 banks, not 4
+    const int wch = KC == 16 ? (l & ~3) | ((l & 3) ^ ((l >> 3) & 3)) : l;
+    if (l < nchw) st16<0>((unsigned)(uintptr_t)(xs + L.xbytes + 16 * wch), pf[PFX]);
+  };
+
+  // accumulators: phase 3's fp32 MFMA chains over the wave's tiles (in AGPRs: no VALU touches
+  // them before the end of the launch, so the 20 block chains run interleaved)
+  f32x4 cacc[NBX], bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int nb = 0; nb < NBX; ++nb) cacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // invalid lanes' stores land in this workgroup's partial row (rewritten at the end of the launch;
+  // the host guarantees k(F+k) >= 1024 doubles): every wave tile issues exactly NSTB stores per lane
+  float* dummy = reinterpret_cast<float*>(partials + (size_t)blockIdx.x * k * (F + k)) + 64 * w + l;
+  STAMP_DECL
+  EOI_DECL
+
+  // phase 1 for a PAIR of wave tiles: each K-step's three H terms are read from LDS once for both
+  // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body)
+  auto phase1 = [&](double (&n0)[4], double (&n1)[4]) {
+    const unsigned char* xa0 = xsp[0] + li * XR + 16 * g;
+    const unsigned char* xa1 = xsp[1] + li * XR + 16 * g;
+    const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
+#pragma unroll
+    for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
+      if (!KSC && ks >= KS) break;
+      const s16x8 a = *reinterpret_cast<const s16x8*>(xa0 + 64 * ks);  // 16-B aligned rows: one b128
+      const s16x8 c = *reinterpret_cast<const s16x8*>(xa1 + 64 * ks);
+      const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
+      const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
+      const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
+      const bf16x8 av = __builtin_bit_cast(bf16x8, a), cv = __builtin_bit_cast(bf16x8, c);
+      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f}, v = f32x4{0.f, 0.f, 0.f, 0.f};
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b2, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b2, v, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, u, 0, 0, 0);
+      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b1, v, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        n0[r] += (double)u[r];
+        n1[r] += (double)v[r];
+      }
+    }
+  };
+  // phases 2 and 3 of one wave tile (slot p, first row r0; invalid: w' = 0 and dummy stores)
+  auto update = [&](int p, int64_t r0, bool valid, const double (&num64)[4]) {
+    const unsigned char* xs = xsp[p];
+    const float* wso = reinterpret_cast<const float*>(xs + L.xbytes);
+    auto wix = [&](int s, int m) { return KC == 16 ? 16 * s + (m ^ (((s >> 1) & 3) << 2)) : s * k + m; };
+    // phase 2: den = w·HHᵀ (f64 MFMA; A row ρ = li carries sample 4(ρ&3) + (ρ>>2), so D[g + 4r] is
+    // sample 4g + r), then w' = w·num/den (SK:553-629) for (s = 4g + r, n = li)
+    f64x4 den = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int sa = 4 * (li & 3) + (li >> 2);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int m = 4 * kk + g;
+      const double av = m < k ? (double)wso[wix(sa, m)] : 0.0;
+      den = __builtin_amdgcn_mfma_f64_16x16x4f64(av, hhb[kk], den, 0, 0, 0);
+    }
+    float wr[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int s = 4 * g + r;
+      float wn = 0.f;
+      if (li < k) {
+        double d = den[r];
+        const double wold = (double)wso[wix(s, li)];
+        if (l1 > 0.0) d += l1;              // SK:616-617
+        if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
+        if (d == 0.0) d = EPS32;            // SK:620
+        wn = (float)(wold * (num64[r] / d));  // SK:622-629
+      }
+      wn = valid ? wn : 0.f;
+      wr[r] = wn;
+      float* dst = (valid && li < k) ? W + (size_t)(r0 + s) * k + li : dummy + 256 * (r + 4 * p);
+      *dst = wn;
+    }
+    if (!do_acc) return;
+    // phase 3: A[m = 4g + r][f = 16nb + li] and B[m][n] over the tile's 16 samples
+    s16x4 a1, a2, a3;  // w'[4g + j][li] in three bf16 terms: the A operand (row m = li, k = 4g + j)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint16_t h1 = bm::bf16_rn(wr[j]);
+      const float r1 = wr[j] - bm::bf16_f(h1);
+      const uint16_t h2 = bm::bf16_rn(r1);
+      const float r2 = r1 - bm::bf16_f(h2);
+      a1[j] = (short)h1;
+      a2[j] = (short)h2;
+      a3[j] = (short)bm::bf16_rn(r2);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
+    const int q = li >> 2, pp = li & 3;
+    const unsigned char* xb0 = xs + (4 * g + q) * XR + 8 * pp;
+#pragma unroll
+    for (int nb = 0; nb < NBX; ++nb) {
+      if (nb < (KSC ? 2 * KSC : NB)) {
+        const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb0 + 32 * nb));
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a3, b, cacc[nb], 0, 0, 0);
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, b, cacc[nb], 0, 0, 0);
+        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, b, cacc[nb], 0, 0, 0);
+      }
+    }
+  };
+
+  u32x4 pf[PD][PFS];
+  static_assert(PD == 2, "a pair of wave tiles per body");
+  static_assert(!PERSIST || (KSC == 10 && KC == 16), "the persistent form serves the cfg4 shape");
+  const int np2 = (ntw + 1) & ~1;  // this wave's tiles per iteration rounded up to whole pairs
+  prefetch(pf[0], 0);
+  prefetch(pf[1], 1);
+#pragma unroll
+  for (int d = 0; d < 2 * NSTB; ++d)  // as if a body had run: the first waits count exactly
+    asm volatile("global_store_dword %0, %1, off" ::"v"(dummy + 256 * d), "v"(0) : "memory");
+  // PERSIST: the end-of-iteration scratch — the waves' sums, then AB, at LDS offset 0 (the slots and
+  // the H terms are rebuilt before the next body stages anything), the reduce-scatter's row-chunk
+  // sums after AB, the control words after the fp64 basis
+  int* sFlag = reinterpret_cast<int*>(smem + L.total + align16((size_t)k * F * 8));
+  double* red2 = reinterpret_cast<double*>(smem + align16((size_t)k * (F + k) * 8));
+  const int n_it = PERSIST ? a.n_iter : 1;
+  for (int it = 0; it < n_it; ++it) {
+    for (int i0 = 0; i0 < ntw; i0 += 2) {
+      STAMP(0);
+      // younger than set 0: set 1's loads and the previous body's 2·NSTB stores; than set 1: the stores
+      wait_set<PFS + 2 * NSTB>(pf[0]);
+      stage(pf[0], xsp[0]);
+      wait_set<2 * NSTB>(pf[1]);
+      stage(pf[1], xsp[1]);
+      STAMP(1);  // 1: waits + staging
+      // the next body's pair; PERSIST, after the iteration's last body: the next iteration's first
+      // pair (the same tiles: their W' of this iteration was stored >= 2 bodies earlier and has
+      // retired at this body's waits — the host keeps >= 6 tiles per workgroup)
+      const int nx = (PERSIST && i0 + 2 >= np2) ? 0 : i0 + 2;
+      prefetch(pf[0], nx);
+      prefetch(pf[1], nx + 1);
+      STAMP(2);  // 2: prefetch issue
+      double n0[4] = {0.0, 0.0, 0.0, 0.0}, n1[4] = {0.0, 0.0, 0.0, 0.0};
+      phase1(n0, n1);
+      STAMP(3);  // 3: phase 1 (both tiles)
+      update(0, row0(i0), true, n0);
+      STAMP(4);  // 4: phases 2 + 3 of the first tile
+      update(1, row0(i0 + 1), i0 + 1 < ntw, n1);
+      STAMP(5);  // 5: phases 2 + 3 of the second tile
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no load outlives the workgroup / the iteration
+    if (!do_acc) {
+      STAMP_FLUSH;
+      return;
+    }
+
+    if (PERSIST) EOI(0);
+    // ---- the workgroup's partial row [k][F + k]: the waves' sums in the order (w0 + w2) + (w1 + w3),
+    // through LDS in two chunks of feature blocks (no per-lane array of sums: the next iteration's
+    // prefetch stays in its AGPRs), [wave][block of the chunk][r][lane] doubles from offset 0
+    __syncthreads();  // every wave done with its slot: LDS is reused from offset 0
+    double* red = reinterpret_cast<double*>(smem);
+    const int V = F + k;
+    double* prow = partials + (size_t)blockIdx.x * k * V;
+    constexpr int NBT = NBX + 1, CH = (NBT + 1) / 2;  // 21 blocks (the last: B = W'ᵀW'), 11 per chunk
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch) {
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const int nb = ch * CH + q;
+        if (nb < NBT)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            red[((w * CH + q) * 4 + r) * 64 + l] = (double)(nb < NBX ? cacc[nb < NBX ? nb : 0][r] : bacc[r]);
+      }
+      __syncthreads();
+      for (int o = t; o < CH * 4 * 64; o += NT) {
+        const int q = o >> 8, r = (o >> 6) & 3, ln = o & 63;
+        const int nb = ch * CH + q;
+        if (nb >= NBT) continue;
+        const int i0 = (q * 4 + r) * 64 + ln, WS = CH * 4 * 64;
+        const double v = (red[i0] + red[2 * WS + i0]) + (red[WS + i0] + red[3 * WS + i0]);
+        const int m = 4 * (ln >> 4) + r, lli = ln & 15;
+        double* dst = nullptr;
+        if (nb < NBX) {
+          const int f = 16 * nb + lli;
+          if (m < k && f < F) dst = prow + (size_t)m * V + f;
+        } else if (m < k && lli < k) {
+          dst = prow + (size_t)m * V + F + lli;
+        }
+        if (dst) {
+          if (PERSIST) st_sc1(dst, v);  // read by other workgroups (any XCD) after barrier A
+          else *dst = v;
+        }
+      }
+      __syncthreads();
+    }
+    if constexpr (!PERSIST) {
+      STAMP_FLUSH;
+      return;
+    } else {
+      // ---- the end of an iteration (PERSIST).  (1) barrier A: every workgroup's partial row stored
+      // (CNT_GROUP0 reaches (it + 1)·G); (2) reduce-scatter: workgroup b sums AB's columns
+      // [b·CW, b·CW + CW) over the G rows in row order (row chunks, then the chunks in order) and
+      // stores them; barrier B (CNT_TOP); (3) every workgroup loads AB and applies the basis update
+      // (SK:634-728, fp64) to its copy of the basis in LDS — the same bits everywhere.  The last
+      // iteration: only the workgroup whose barrier-B add came last applies the update, writes
+      // H64 / Hᵀ / HHᵀ and zeroes the counters; the others leave.  Every wait is bounded (2 s)
+      // and sets the error word (MI355X_MICROARCH.md valid forms row 1: sc1 stores, every storing
+      // wave's vmcnt(0), a barrier, one lane's agent-scope add; sc1 polls and sc1 loads).
+      const int NOUT = k * V;
+      const int Gi = (int)G, b = (int)blockIdx.x;
+      uint32_t* cA = a.cnt + CNT_GROUP0;
+      uint32_t* cB = a.cnt + CNT_TOP;
+      uint32_t* err = a.cnt + CNT_ERR;
+      auto grid_wait = [&](uint32_t* c, uint32_t target, int slot) -> bool {
+        if (t == 0) {
+          int ok = 1;
+          const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+          while (true) {  // the counter and the error word in one batch: one round trip per round
+            const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+            if (ev != 0u) {
+              ok = 0;
+              break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > sl::SPIN_TIMEOUT) {
+              __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = 0;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          sFlag[slot] = ok;
+        }
+        __syncthreads();
+        return sFlag[slot] != 0;
+      };
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      EOI(1);  // 1: the waves' sums -> the partial row, stored
+      if (t == 0) __hip_atomic_fetch_add(cA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!grid_wait(cA, (uint32_t)((it + 1) * Gi), 0)) return;
+      EOI(2);  // 2: barrier A
+      // (2) this workgroup's columns of AB
+      const int CW = (NOUT + Gi - 1) / Gi;
+      const int c0 = b * CW;
+      const int ncols = max(0, min(CW, NOUT - c0));
+      if (CW <= NT) {
+        const int nrc = NT / CW;                // row chunks
+        const int RPC = (Gi + nrc - 1) / nrc;   // rows per chunk
+        const int c = t % CW, r = t / CW;
+        double v = 0.0;
+        if (r < nrc && c < ncols) {
+          // every row of the chunk in ONE batch of loads (sc1 loads are not re-ordered by the
+          // compiler: a loop of dependent batches pays the cross-XCD latency once per batch)
+          const int r0 = r * RPC, r1 = min(Gi, r0 + RPC);
+          for (int m = r0; m < r1; m += 24) {
+            double x[24];
+#pragma unroll
+            for (int u = 0; u < 24; ++u) x[u] = ld_sc1(partials + (size_t)min(m + u, r1 - 1) * NOUT + c0 + c);
+#pragma unroll
+            for (int u = 0; u < 24; ++u) v += m + u < r1 ? x[u] : 0.0;
+          }
+        }
+        if (r < nrc) red2[r * CW + c] = v;
+        __syncthreads();
+        if (t < ncols) {
+          double sum = 0.0;
+          for (int q = 0; q < nrc; ++q) sum += red2[q * CW + t];
+          st_sc1(a.AB + c0 + t, sum);
+        }
+      } else {
+        for (int c = t; c < ncols; c += NT) {
+          double v = 0.0;
+          for (int m = 0; m < Gi; m += 8) {
+            double x[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = ld_sc1(partials + (size_t)min(m + u, Gi - 1) * NOUT + c0 + c);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v += m + u < Gi ? x[u] : 0.0;
+          }
+          st_sc1(a.AB + c0 + c, v);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      EOI(3);  // 3: reduce-scatter
+      const bool last_it = it + 1 == a.n_iter;
+      if (t == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(cB, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag[2] = old == (uint32_t)(a.n_iter * Gi - 1);
+      }
+      __syncthreads();
+      if (last_it) {
+        if (!sFlag[2]) return;  // another workgroup finishes the launch
+      } else if (!grid_wait(cB, (uint32_t)((it + 1) * Gi), 1)) {
+        return;
+      }
+      EOI(4);  // 4: barrier B
+      // (3) the basis update from AB (SK:634-728; wt_update_basis's arithmetic)
+      double* sAB = reinterpret_cast<double*>(smem);
+      for (int o0 = 0; o0 < NOUT; o0 += 12 * NT) {  // batches of 12 loads per thread in flight
+        double x[12];
+#pragma unroll
+        for (int u = 0; u < 12; ++u) x[u] = ld_sc1(a.AB + min(o0 + t + NT * u, NOUT - 1));
+#pragma unroll
+        for (int u = 0; u < 12; ++u)
+          if (o0 + t + NT * u < NOUT) sAB[o0 + t + NT * u] = x[u];
+      }
+      __syncthreads();
+      EOI(5);  // 5: AB -> LDS
+      const int KF = k * F;
+      double* hnew = red2 + NT;  // the new basis, then copied over the old one
+      for (int e = t; e < KF; e += NT) {
+        const int j = e / F;
+        const int f = e - j * F;
+        const double h = sH64[e];
+        const double num = sAB[j * V + f];                                             // SK:639
+        double den = 0.0;                                                              // SK:640
+        for (int m = 0; m < k; ++m) den = fma(sAB[j * V + F + m], sH64[m * F + f], den);
+        if (a.l1H > 0.0) den += a.l1H;                                                 // SK:702-703
+        if (a.l2H > 0.0) den = den + a.l2H * h;                                        // SK:704-705
+        if (den == 0.0) den = EPS32;                                                   // SK:706
+        hnew[e] = h * (num / den);                                                     // SK:722-726
+      }
+      __syncthreads();
+      for (int e = t; e < KF; e += NT) sH64[e] = hnew[e];
+      __syncthreads();
+      EOI(6);  // 6: the update
+      derive();
+      if (last_it) {  // the basis state for the host, the counters back at rest
+        __syncthreads();
+        for (int e = t; e < KF; e += NT) a.H64[e] = sH64[e];
+        for (int e = t; e < F * bm::KP; e += NT) {
+          const int f = e / bm::KP, n = e - f * bm::KP;
+          a.Ht_out[e] = n < k ? sH64[n * F + f] : 0.0;
+        }
+        a.HHt_out[t] = sHHt[t];
+        if (t == 0) {
+          __hip_atomic_store(cA, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(cB, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+      zero_pads();
+      __syncthreads();
+      EOI(7);  // 7: H terms, HHᵀ, pads
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * bm::KP + li];
+#pragma unroll
+      for (int nb = 0; nb < NBX; ++nb) cacc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      bacc = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+template <int KSC, int KC>
+__global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __restrict__ X, float* __restrict__ W,
+                                                            const double* __restrict__ Ht,
+                                                            const double* __restrict__ HHt,
+                                                            double* __restrict__ partials, int64_t n_rows, int F,
+                                                            int k, double l1, double l2, int flags,
+                                                            int64_t n_tiles) {
+  BfwArgs a{};
+  a.X = X;
+  a.W = W;
+  a.Ht = Ht;
+  a.HHt = HHt;
+  a.partials = partials;
+  a.n_rows = n_rows;
+  a.F = F;
+  a.k = k;
+  a.l1 = l1;
+  a.l2 = l2;
+  a.flags = flags;
+  a.n_tiles = n_tiles;
+  bfw_run<KSC, KC, false>(a);
+}
+
+// ------------------------------------------------------------------------------------------------
+// mu_iter_bfw_kernel — cfg4 (bf16 X, F = 289..320, k = 16) as ONE persistent launch of n MU
+// iterations: the wave-tile pass above with the cross-workgroup reduction and
+// the basis update inside the launch, so an iteration has no kernel boundary, no separate
+// reduction / update launch and no launch gap.  The next iteration's first pair of tiles is already
+// in flight (AGPRs) while the workgroups meet; every workgroup keeps its own fp64 copy of the basis
+// in LDS.  One workgroup per CU (the grid co-resident: the host checks the occupancy query).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT, 1) void mu_iter_bfw_kernel(BfwArgs a) { bfw_run<10, 16, true>(a); }
 
 // out[o] = Σ_m rows[m][o] in m order for the rows m = m0, m0 + step, ... (cnt rows); sc1 loads.
 // Batches of 16 rows for both of a thread's outputs are issued before any is summed (row index
@@ -5291,6 +5570,29 @@ static int64_t max_resident(PassFn fn, size_t lds) {
   return v;
 }
 
+// the persistent cfg4 launch (mu_iter_bfw_kernel): bf16 X, F with 10 K-steps (289..320), k = 16,
+// whole 64-sample tiles, >= 6 wave-tile pairs' worth of tiles per workgroup (the prefetch of the
+// next iteration's first pair must find its W' retired), the grid co-resident.  CNMF_BFW_PERSIST=0
+// (diagnostic build) keeps the per-iteration launches for A/B runs.
+struct BwpLaunch {
+  int64_t G, n_tiles;
+  size_t lds;
+};
+static bool bwp_plan(int64_t n_rows, int x_dtype, int F, int k, BwpLaunch* out) {
+  if (!use_bfw(x_dtype, F, k) || bm::ksteps(F) != 10 || k != 16 || n_rows <= 0 || n_rows % TS != 0) return false;
+  if (diag_env("CNMF_BFW_PERSIST") && atoi(diag_env("CNMF_BFW_PERSIST")) == 0) return false;
+  const size_t lds = (size_t)bw::lds(F).total + align16((size_t)k * F * 8) + 16;
+  if (lds > kMaxLds) return false;
+  const int64_t n_tiles = n_rows / TS;
+  const int64_t cap = max_resident(reinterpret_cast<PassFn>(&mu_iter_bfw_kernel), lds);
+  int64_t G = std::min<int64_t>(cap, n_tiles / 7);
+  if (G < 1) return false;
+  const int64_t rounds = (n_tiles + G - 1) / G;  // >= 7: every workgroup >= 6 tiles
+  G = (n_tiles + rounds - 1) / rounds;
+  *out = BwpLaunch{G, n_tiles, lds};
+  return true;
+}
+
 static int64_t pass_grid(int64_t n_rows, PassFn fn, size_t lds) {
   const int64_t n_tiles = (n_rows + TS - 1) / TS;
   if (n_tiles == 0) return 0;
@@ -6300,7 +6602,9 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
   wa_derive(smem, t, delta2);
 }
 
-template <int PD, int OCC, bool MULTI = false>
+// HREG (diagnostic A/B, one workgroup per CU): the lane's fp64 Hᵀ rows held in VGPRs for the
+// iteration instead of re-read from LDS every tile (42 ds_read_b128 per wave tile)
+template <int PD, int OCC, bool MULTI = false, bool HREG = false>
 __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
@@ -6339,6 +6643,16 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   if (l < G4::PADB / 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
   __syncthreads();
   wa_derive(smem, t, a.delta2);
+  double hreg[HREG ? NQ : 1][KK];
+  auto load_h = [&]() {
+    if constexpr (HREG) {
+#pragma unroll
+      for (int c = 0; c < NQ; ++c)
+#pragma unroll
+        for (int j = 0; j < KK; ++j) hreg[c][j] = sHtl[c * KK + j];
+    }
+  };
+  load_h();
 
   f2 acc[NQ][KP], accB[KP];
   auto zero_acc = [&]() {
@@ -6400,8 +6714,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     double cc[KK] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
-      const double2 h01 = *reinterpret_cast<const double2*>(sHtl + c * KK);
-      const double2 h23 = *reinterpret_cast<const double2*>(sHtl + c * KK + 2);
+      const double2 h01 = HREG ? make_double2(hreg[HREG ? c : 0][0], hreg[HREG ? c : 0][1])
+                               : *reinterpret_cast<const double2*>(sHtl + c * KK);
+      const double2 h23 = HREG ? make_double2(hreg[HREG ? c : 0][2], hreg[HREG ? c : 0][3])
+                               : *reinterpret_cast<const double2*>(sHtl + c * KK + 2);
       const double x = (double)xv[c];
       cc[0] = fma(x, h01.x, cc[0]);
       cc[1] = fma(x, h01.y, cc[1]);
@@ -6570,6 +6886,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       __syncthreads();
     }
     wa_update_basis(t, a.lam, a.delta2);
+    load_h();
     TL(it, 1);
   };
 
@@ -6977,6 +7294,14 @@ int cnmf_debug_xtimeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
   return CNMF_OK;
 }
+int cnmf_debug_eoi(unsigned long long* host_out, int reset) {  // [16]: persistent bfw end-of-iteration phases
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_eoi), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_eoi), z, sizeof(z)));
+  }
+  return CNMF_OK;
+}
 int cnmf_debug_stamps(unsigned long long* host_out, int reset) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16));
   if (reset) {
@@ -7257,17 +7582,24 @@ struct WaLaunch {
 // workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2, default 2: two waves per SIMD hide the
 // fp64 and LDS latencies of the W-step, at 256 registers per lane and PD = 2; measured on one box,
 // cfg5: 146.6 us per iteration at 1, 123.1 us at 2, profiles/r02/session5/als_iter)
-static int wa_occ() {
-  static const int v = diag_env("CNMF_ALS_OCC") && atoi(diag_env("CNMF_ALS_OCC")) == 1 ? 1 : 2;
-  return v;
+// (diagnostic build: CNMF_ALS_OCC=1 one workgroup per CU, =3 one per CU with Hᵀ in VGPRs (HREG))
+static int wa_variant() {
+  static const int v = diag_env("CNMF_ALS_OCC") ? atoi(diag_env("CNMF_ALS_OCC")) : 2;
+  return (v == 1 || v == 3) ? v : 2;
 }
+static int wa_occ() { return wa_variant() == 2 ? 2 : 1; }
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
 static PassFn wa_fn(bool multi = false) {
-  if (multi)
-    return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true>)
-                         : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>);
-  return wa_occ() == 1 ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1>)
-                       : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
+#ifdef CNMF_DIAG
+  if (wa_variant() == 1)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1>);
+  if (wa_variant() == 3)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, false, true>);
+#endif
+  return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>)
+               : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
 }
 static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false) {
   const int PD = wa_pd();
@@ -7388,6 +7720,8 @@ int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dty
   // multi: bit 0 = the in-launch exchange form, bit 1 = the device tolerance test's (TOL) kernel
   if (wt_plan(n_rows, x_dtype, n_features, k, (multi & 1) != 0, layout, &L, (multi & 2) != 0)) return L.G;
   if (multi & 2) return 0;  // cnmf_mu_fit_tol serves the wave tiles only
+  BwpLaunch B;
+  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) return (multi & 1) ? 0 : B.G;  // cfg4: one GPU only
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k, (multi & 1) != 0);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : g;
 }
@@ -7395,6 +7729,8 @@ int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dty
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   WtLaunch L;
   if (wt_plan(n_rows, x_dtype, n_features, k, false, 4, &L)) return 1;
+  BwpLaunch B;
+  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) return 1;
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
 }
@@ -7417,6 +7753,14 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
                "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
                "(%lld workgroups), no barrier inside an iteration",
                k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
+    return 1;
+  }
+  BwpLaunch B;
+  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) {
+    snprintf(out, (size_t)len,
+             "mu_iter_bfw_kernel<k=16, F=%d>: bf16 matrix-core wave tiles, one 4-wave workgroup per CU (%lld "
+             "workgroups), reduction and basis update in the launch",
+             n_features, (long long)B.G);
     return 1;
   }
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
@@ -7696,6 +8040,42 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
       return CNMF_OK;
     }
   }
+  {  // cfg4: the bf16 wave-tile pass with the reduction and the basis update in the launch
+    BwpLaunch B;
+    if (bwp_plan(n_rows, x_dtype, n_features, k, &B) && B.G <= n_parts) {
+      if (!X || !W || !H64 || !Ht || !HHt || !partials || !counter || !AB)
+        return set_err(CNMF_ERR_ARG, "null pointer argument");
+      if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
+        return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
+      BfwArgs ba{};
+      ba.X = static_cast<const bf16_t*>(X);
+      ba.W = static_cast<float*>(W);
+      ba.Ht = Ht;
+      ba.HHt = HHt;
+      ba.partials = partials;
+      ba.n_rows = n_rows;
+      ba.F = n_features;
+      ba.k = k;
+      ba.l1 = l1_W;
+      ba.l2 = l2_W;
+      ba.flags = CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE;
+      ba.n_tiles = B.n_tiles;
+      ba.H64 = H64;
+      ba.Ht_out = Ht;
+      ba.HHt_out = HHt;
+      ba.AB = AB;
+      ba.cnt = counter;
+      ba.n_iter = n_iter;
+      ba.l1H = l1_H;
+      ba.l2H = l2_H;
+      void* args[] = {&ba};
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
+      HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(&mu_iter_bfw_kernel), dim3((unsigned)B.G), dim3(NT),
+                                args, B.lds, hs));
+      if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+      return CNMF_OK;
+    }
+  }
   const int64_t G = persist_grid(n_rows, x_dtype, n_features, k);
   if (G < 0) return set_err(CNMF_ERR_HIP, "occupancy query failed");
   if (G > 0) {
@@ -7711,15 +8091,15 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
     return CNMF_OK;
   }
   const bool ev = events && n_events >= 2 * n_iter;
-  for (int it = 0; it < n_iter; ++it) {
+  for (int it = 0; it < n_iter; ++it) {  // events around the whole iteration (pass + reduction + update)
     if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it]), hs));
     int st = cnmf_mu_sample_pass(X, x_dtype, W, Ht, HHt, partials, n_rows, n_features, k, l1_W,
                                  l2_W, CNMF_PASS_UPDATE_W | CNMF_PASS_ACCUMULATE, stream);
     if (st) return st;
-    if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it + 1]), hs));
     st = cnmf_reduce_update(partials, n_parts, stage, counter, AB, H64, Ht, HHt, n_features, k, l1_H,
                             l2_H, stats, stream);
     if (st) return st;
+    if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it + 1]), hs));
   }
   return CNMF_OK;
 }

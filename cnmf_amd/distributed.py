@@ -92,7 +92,7 @@ def factorise_sharded(X_shard, W_shard, H0, *, max_iter=200, tol=1e-4, l1_reg_W=
     if exchange == "auto" and update_H:
         # every rank must take the same decision before the collective enable_exchange
         from .solver import agree_max
-        if agree_max([0.0 if plan.persistent_shape else 1.0], group, plan.device)[0] != 0.0:
+        if agree_max([0.0 if plan.exchange_shape else 1.0], group, plan.device)[0] != 0.0:
             exchange = False
     if exchange and update_H:
         try:

@@ -110,7 +110,7 @@ def _exchange_fits(plans, shared_device_exchange=False) -> bool:
     """Every shard a persistent shape, and on each device the shards' persistent grids together
     within the CUs (one resident wave-tile workgroup per CU): co-running launches on one device all
     have to be resident, or the exchange would wait for a launch that cannot start."""
-    if not all(getattr(p, "persistent_shape", False) for p in plans):
+    if not all(getattr(p, "exchange_shape", False) for p in plans):
         return False
     if len({p.device.index for p in plans}) < len(plans) and not shared_device_exchange:
         return False

@@ -132,6 +132,10 @@ class MUPlan:
         with torch.cuda.device(self.device):
             p = self.lib.cnmf_mu_persistent(self.n_rows, self.F, self.k, self.xdt)
         self.persistent_shape = bool(check(p, "cnmf_mu_persistent"))  # the persistent kernel serves it
+        # ...and its in-launch cross-rank exchange (the wave-tile shapes; cfg4's bf16 launch is one GPU only)
+        with torch.cuda.device(self.device):
+            xg = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, 0, 1) if self.persistent_shape else 0
+        self.exchange_shape = self.persistent_shape and int(xg) > 0
         self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
         self.layout = 0  # layout of the persistent launch (include/cnmf_hip.h; 0 = default); tune() sets it
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
@@ -155,7 +159,7 @@ class MUPlan:
         if getattr(self.group, "is_local", False):
             return self._enable_exchange_local()
         rank = dist.get_rank(self.group)
-        ok = torch.tensor([1.0 if self.persistent_shape else 0.0])
+        ok = torch.tensor([1.0 if self.exchange_shape else 0.0])
         handle, ptr, err = None, ctypes.c_void_p(), ""
         # peer reachability first: every peer's GPU that this process can see must be mappable
         devs = [None] * self.world
@@ -166,7 +170,7 @@ class MUPlan:
             if r != rank and j is not None and j != self.device.index and \
                     self.lib.cnmf_device_can_access_peer(self.device.index, j) != 1:
                 ok[0], err = 0.0, f"no peer access from device {self.device.index} to {j} ({bus})"
-        if self.persistent_shape and ok[0] != 0.0:
+        if self.exchange_shape and ok[0] != 0.0:
             hb = int(self.lib.cnmf_xbuf_handle_bytes())
             hbuf = ctypes.create_string_buffer(hb)
             with torch.cuda.device(self.device):
@@ -219,8 +223,8 @@ class MUPlan:
         Collective over the local group: raises on every shard when any shard cannot take part."""
         grp = self.group
         ptr, err = ctypes.c_void_p(), ""
-        if not self.persistent_shape:
-            err = f"shard {grp.rank()}: not a persistent shape"
+        if not self.exchange_shape:
+            err = f"shard {grp.rank()}: not a persistent shape with the in-launch exchange"
         else:
             hbuf = ctypes.create_string_buffer(int(self.lib.cnmf_xbuf_handle_bytes()))
             with torch.cuda.device(self.device):
@@ -717,6 +721,7 @@ class ALSPlan(MUPlan):
             p = self.lib.cnmf_als_persistent(self.n_rows, self.F, self.k, self.xdt)
         # one persistent launch per stretch of iterations (als_iter_wt_kernel), single GPU
         self.persistent_shape = bool(check(p, "cnmf_als_persistent"))
+        self.exchange_shape = self.persistent_shape
         self.persistent = self.persistent_shape and self.world == 1
 
     def refresh_basis(self):
@@ -815,7 +820,7 @@ class WeightedMUPlan:
     `cnmf_wmu_persistent`): n iterations are ONE launch of the persistent weighted kernel
     (`cnmf_wmu_iterations`: pass, in-launch reduction and H-step per iteration)."""
 
-    persistent = persistent_shape = exchange = False
+    persistent = persistent_shape = exchange_shape = exchange = False
 
     def __init__(self, X: torch.Tensor, M: torch.Tensor, n_components: int, group=None):
         self.lib = _lib.load()
@@ -849,6 +854,7 @@ class WeightedMUPlan:
         with torch.cuda.device(self.device):
             p = self.lib.cnmf_wmu_persistent(self.n_rows, self.F, self.k)
         self.persistent_shape = bool(check(p, "cnmf_wmu_persistent"))
+        self.exchange_shape = self.persistent_shape
         self.persistent = self.persistent_shape and self.world == 1
 
     def _stream(self):

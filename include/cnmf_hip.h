@@ -123,7 +123,11 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  * Other shapes: pass + reduce_update per iteration.
  * events (may be NULL), caller-created hipEvent_t recorded on `stream` for live kernel timing:
  *   persistent: events[0] / events[1] before / after the launch (n_events >= 2);
- *   otherwise : events[2i] / events[2i+1] around sample pass i (n_events >= 2*n_iter). */
+ *   otherwise : events[2i] / events[2i+1] around iteration i: its pass, reduction and basis
+ *               update (n_events >= 2*n_iter).
+ * Persistent shapes: fp32 F = 81, k = 4 / 8 (mu_iter_wt_kernel) and bf16 F = 289..320, k = 16
+ * with n_rows a multiple of 64 (mu_iter_bfw_kernel, cfg4: the reduction and the update inside the
+ * launch too). */
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,

@@ -33,7 +33,7 @@ def _run_two_ranks(extra, timeout=240):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
                    LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-               "--steps", "20", "--warmup", "20", "--no-cpu", "--ramp-seconds", "0.2"] + extra
+               "--steps", "20", "--warmup", "20", "--no-cpu", "--ramp-seconds", "0.2", "--scaling", "strong"] + extra
         procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -72,3 +72,15 @@ def test_bench_two_ranks_one_gpu_host_collective_path():
     assert res["n_gpus"] == 2 and res["value"] > 0
     assert res["config"]["exchange"] is None
     assert res["roofline"]["launches_timed"] == 20
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_one_gpu_weak_scaling():
+    """The default scaling (weak): every rank owns --rows rows; the line's value is the 1e6-row
+    iterations all ranks completed per second, the exchange validated as at strong scaling."""
+    res, _ = _run_two_ranks(["--rows", "16384", "--scaling", "weak"])
+    assert res["scaling"] == "weak" and res["n_gpus"] == 2
+    assert res["config"]["n_rows_per_gpu"] == 16384 and res["config"]["n_rows_total"] == 32768
+    assert res["config"]["exchange"].startswith("validated"), res["config"]["exchange"]
+    it_s = res["steps"] / (res["ms_per_step"] * res["steps"] / 1e3)
+    assert abs(res["value"] - 2 * 16384 / 1e6 * it_s) <= 0.02 * res["value"]

@@ -149,3 +149,26 @@ def test_wave_tiles_streamed_w_k4():
                               max_iter=30, tol=0.0)
     W, H = a.W.cpu().numpy(), a.H64.cpu().numpy()
     assert rel_fro(W, Wr) <= TOL32 and rel_fro(H, Hr) <= TOL32, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+@pytest.mark.timeout(900)
+def test_cfg3_full_shard_k8_500_iterations():
+    """cfg3's per-GPU shard (1.25e6 x 81, k = 8, W streamed with X) for the config's 500 iterations
+    against the fp64 oracle (k = 8 at 500 iterations was pinned only at 50,000 rows)."""
+    import torch
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    N = 1_250_000
+    X = iop_spectra(N, 81, seed=5, dtype=np.float32)
+    W0, H0 = random_init(X, 8, 42)
+    plan = _plan(X, W0, H0)
+    assert plan.persistent and "streamed" in plan.describe(), plan.describe()
+    for _ in range(5):
+        plan.iterate(100)
+    torch.cuda.synchronize()
+    plan.check_sync_error()
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=500, tol=0.0)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    ew, eh = rel_fro(W, Wr), rel_fro(H, Hr)
+    print(f"cfg3 shard 1.25e6 x 81 k8, 500 it: rel W {ew:.2e} rel H {eh:.2e}")
+    assert ew <= TOL32 and eh <= TOL32, (ew, eh)

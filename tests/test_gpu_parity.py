@@ -60,7 +60,7 @@ def test_golden_case_through_api(name):
     assert ew <= tol and eh <= tol, (name, ew, eh)
     # and against sklearn's own outputs on the same inputs (fp32 sklearn drifts from fp64 itself:
     # the measured distance is printed, and recorded by tools/parity_report.py)
-    ref_tol = TOL64 if X.dtype == np.float64 else 5e-5
+    ref_tol = TOL64 if X.dtype == np.float64 else 1.2e-5  # measured <= 9.0e-6 (sklearn fp32's own drift)
     esw, esh = rel_fro(W, case["W"]), rel_fro(H, case["H"])
     skw, skh = rel_fro(case["W"], Wr), rel_fro(case["H"], Hr)
     print(f"{name}: GPU vs fp64 oracle W {ew:.2e} H {eh:.2e}; GPU vs sklearn W {esw:.2e} H {esh:.2e}; "

@@ -56,7 +56,7 @@ def test_default_fit_matches_sklearn(name):
     print(f"{name}: n_iter {n}; GPU vs fp64 oracle W {ew64:.2e} H {eh64:.2e}; GPU vs sklearn fp32 "
           f"W {ew:.2e} H {eh:.2e}; sklearn fp32 vs fp64 oracle W {ew_sk:.2e} H {eh_sk:.2e}")
     assert ew64 <= 1e-5 and eh64 <= 1e-5, (ew64, eh64)
-    assert ew <= 2e-5 and eh <= 2e-5, (ew, eh)
+    assert ew <= 1.2e-5 and eh <= 1.2e-5, (ew, eh)  # measured 7.4e-6 = sklearn fp32's own drift
 
 
 def test_gpu_init_distance_is_stated():

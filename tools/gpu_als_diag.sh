@@ -4,7 +4,7 @@
 # als_iter_wt_kernel (each its own run, kernel-trace only).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-D=gpurun_out/als_diag2
+D=gpurun_out/${1:-als_diag}
 mkdir -p $D
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 P="timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv"

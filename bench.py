@@ -439,8 +439,8 @@ def main():
     # the same layout
     tuned = {}
     if args.layout > 0 and args.solver == "mu" and not args.weighted:
-        plan.layout = args.layout
-    elif args.solver == "mu" and plan.persistent and not args.no_tune and not args.weighted:
+        plan.set_layout(args.layout)
+    elif args.solver == "mu" and getattr(plan, "layouts", ()) and not args.no_tune and not args.weighted:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
     layout = plan.describe() if plan.persistent else None

@@ -2261,6 +2261,13 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// two doubles as one 16-byte sc1 store (p 16-byte aligned; the MI355X guide's table: a 16-B sc1
+// store costs about a plain one, 8-B accesses 0.54-0.70x the rate)
+__device__ __forceinline__ void st16_sc1(double* p, double v0, double v1) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  const d2v v = d2v{v0, v1};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 
 // The arguments of the bf16 wave-tile pass and of its persistent form (mu_iter_bfw_kernel).
 struct BfwArgs {
@@ -2572,23 +2579,33 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
             red[((w * CH + q) * 4 + r) * 64 + l] = (double)(nb < NBX ? cacc[nb < NBX ? nb : 0][r] : bacc[r]);
       }
       __syncthreads();
-      for (int o = t; o < CH * 4 * 64; o += NT) {
+      // two adjacent lanes' values per thread (the same row m, features f and f + 1): one 16-byte
+      // store when both are in the row and the pair is 16-byte aligned, else one 8-byte store each
+      for (int o = 2 * t; o < CH * 4 * 64; o += 2 * NT) {
         const int q = o >> 8, r = (o >> 6) & 3, ln = o & 63;
         const int nb = ch * CH + q;
         if (nb >= NBT) continue;
         const int i0 = (q * 4 + r) * 64 + ln, WS = CH * 4 * 64;
-        const double v = (red[i0] + red[2 * WS + i0]) + (red[WS + i0] + red[3 * WS + i0]);
-        const int m = 4 * (ln >> 4) + r, lli = ln & 15;
-        double* dst = nullptr;
+        double v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          v[h] = (red[i0 + h] + red[2 * WS + i0 + h]) + (red[WS + i0 + h] + red[3 * WS + i0 + h]);
+        const int m = 4 * (ln >> 4) + r, lli = ln & 15;  // lli even
+        int64_t at = -1, lim = 0;  // element offset of lane ln's value in the row, valid count
         if (nb < NBX) {
           const int f = 16 * nb + lli;
-          if (m < k && f < F) dst = prow + (size_t)m * V + f;
+          if (m < k && f < F) at = (int64_t)m * V + f, lim = min(2, F - f);
         } else if (m < k && lli < k) {
-          dst = prow + (size_t)m * V + F + lli;
+          at = (int64_t)m * V + F + lli, lim = min(2, k - lli);
         }
-        if (dst) {
-          if (PERSIST) st_sc1(dst, v);  // read by other workgroups (any XCD) after barrier A
-          else *dst = v;
+        if (at < 0) continue;
+        if (PERSIST) {  // read by other workgroups (any XCD) after barrier A: sc1 stores
+          if (lim == 2 && (at & 1) == 0)
+            st16_sc1(prow + at, v[0], v[1]);
+          else
+            for (int h = 0; h < lim; ++h) st_sc1(prow + at + h, v[h]);
+        } else {
+          for (int h = 0; h < lim; ++h) prow[at + h] = v[h];
         }
       }
       __syncthreads();
@@ -2634,9 +2651,10 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         __syncthreads();
         return sFlag[slot] != 0;
       };
+      EOI(1);  // 1: the waves' sums -> the partial row, stores issued
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      EOI(1);  // 1: the waves' sums -> the partial row, stored
+      EOI(8);  // 8: the row's stores retired
       if (t == 0) __hip_atomic_fetch_add(cA, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (!grid_wait(cA, (uint32_t)((it + 1) * Gi), 0)) return;
       EOI(2);  // 2: barrier A
@@ -2650,15 +2668,15 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         const int c = t % CW, r = t / CW;
         double v = 0.0;
         if (r < nrc && c < ncols) {
-          // every row of the chunk in ONE batch of loads (sc1 loads are not re-ordered by the
-          // compiler: a loop of dependent batches pays the cross-XCD latency once per batch)
+          // the chunk's rows in batches of 11 loads in flight (the compiler does not re-order sc1
+          // loads: every batch pays the cross-XCD latency once)
           const int r0 = r * RPC, r1 = min(Gi, r0 + RPC);
-          for (int m = r0; m < r1; m += 24) {
-            double x[24];
+          for (int m = r0; m < r1; m += 11) {
+            double x[11];
 #pragma unroll
-            for (int u = 0; u < 24; ++u) x[u] = ld_sc1(partials + (size_t)min(m + u, r1 - 1) * NOUT + c0 + c);
+            for (int u = 0; u < 11; ++u) x[u] = ld_sc1(partials + (size_t)min(m + u, r1 - 1) * NOUT + c0 + c);
 #pragma unroll
-            for (int u = 0; u < 24; ++u) v += m + u < r1 ? x[u] : 0.0;
+            for (int u = 0; u < 11; ++u) v += m + u < r1 ? x[u] : 0.0;
           }
         }
         if (r < nrc) red2[r * CW + c] = v;
@@ -2696,39 +2714,83 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         return;
       }
       EOI(4);  // 4: barrier B
-      // (3) the basis update from AB (SK:634-728; wt_update_basis's arithmetic)
+      // (3) the basis update from AB (SK:634-728), basis_update_split_kernel's arithmetic on the f64
+      // matrix cores: wave w takes H's 16-feature blocks nb ≡ w (mod 4) — per block den = (WᵀW)·H
+      // (4 MFMAs, old H), the new block in place, and the block's HHᵀ partial (4 MFMAs) chained over
+      // the wave's blocks in block order; the four waves' partials are summed in a fixed order
       double* sAB = reinterpret_cast<double*>(smem);
-      for (int o0 = 0; o0 < NOUT; o0 += 12 * NT) {  // batches of 12 loads per thread in flight
-        double x[12];
+      for (int o0 = 0; o0 < NOUT; o0 += 11 * NT) {  // AB in batches of 11 loads per thread in flight
+        double x[11];
 #pragma unroll
-        for (int u = 0; u < 12; ++u) x[u] = ld_sc1(a.AB + min(o0 + t + NT * u, NOUT - 1));
+        for (int u = 0; u < 11; ++u) x[u] = ld_sc1(a.AB + min(o0 + t + NT * u, NOUT - 1));
 #pragma unroll
-        for (int u = 0; u < 12; ++u)
+        for (int u = 0; u < 11; ++u)
           if (o0 + t + NT * u < NOUT) sAB[o0 + t + NT * u] = x[u];
       }
       __syncthreads();
       EOI(5);  // 5: AB -> LDS
-      const int KF = k * F;
-      double* hnew = red2 + NT;  // the new basis, then copied over the old one
-      for (int e = t; e < KF; e += NT) {
-        const int j = e / F;
-        const int f = e - j * F;
-        const double h = sH64[e];
-        const double num = sAB[j * V + f];                                             // SK:639
-        double den = 0.0;                                                              // SK:640
-        for (int m = 0; m < k; ++m) den = fma(sAB[j * V + F + m], sH64[m * F + f], den);
-        if (a.l1H > 0.0) den += a.l1H;                                                 // SK:702-703
-        if (a.l2H > 0.0) den = den + a.l2H * h;                                        // SK:704-705
-        if (den == 0.0) den = EPS32;                                                   // SK:706
-        hnew[e] = h * (num / den);                                                     // SK:722-726
+      typedef double f64x4v __attribute__((ext_vector_type(4)));
+      double* sblk = red2 + NT + w * (16 * 17);          // this wave's new block [j][f] (stride 17)
+      double* hpart = red2 + NT + 4 * (16 * 17);         // [wave][16][16] HHᵀ partials
+      {
+        double bfr[4];  // A operand: (WᵀW)[j = li][m = 4kk + g]
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int m = 4 * kk + g;
+          bfr[kk] = (li < k && m < k) ? sAB[li * V + F + m] : 0.0;
+        }
+        f64x4v hh = f64x4v{0.0, 0.0, 0.0, 0.0};
+        const int NBF = (F + 15) / 16;
+        for (int nb = w; nb < NBF; nb += 4) {
+          const int f = 16 * nb + li;
+          const bool fok = f < F;
+          double hb[4], num[4], hold[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int m = 4 * kk + g;
+            hb[kk] = (m < k && fok) ? sH64[m * F + f] : 0.0;  // H[m][f] (old)
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = g + 4 * r;
+            const bool ok = j < k && fok;
+            num[r] = ok ? sAB[j * V + f] : 0.0;  // (WᵀX)[j][f], SK:639
+            hold[r] = ok ? sH64[j * F + f] : 0.0;
+          }
+          f64x4v den = f64x4v{0.0, 0.0, 0.0, 0.0};  // ((WᵀW)·H)[j][f], SK:640
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) den = __builtin_amdgcn_mfma_f64_16x16x4f64(bfr[kk], hb[kk], den, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int j = g + 4 * r;
+            double h = hold[r];
+            if (j < k && fok) {
+              double d = den[r];
+              if (a.l1H > 0.0) d += a.l1H;          // SK:702-703
+              if (a.l2H > 0.0) d = d + a.l2H * h;   // SK:704-705
+              if (d == 0.0) d = EPS32;              // SK:706
+              h = h * (num[r] / d);                 // SK:722-726
+              sH64[j * F + f] = h;
+            }
+            sblk[j * 17 + li] = (j < k && fok) ? h : 0.0;
+          }
+          // this block's HHᵀ: A[j = li][f = 4kk + g] = B[f][m = li] = h[li][4kk + g] (the wave's own
+          // LDS writes above precede these reads)
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const double v = sblk[li * 17 + 4 * kk + g];
+            hh = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, hh, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hpart[(w * 16 + g + 4 * r) * 16 + li] = hh[r];  // P[j = g + 4r][m = li]
       }
       __syncthreads();
-      for (int e = t; e < KF; e += NT) sH64[e] = hnew[e];
+      sHHt[t] = (hpart[t] + hpart[256 + t]) + (hpart[512 + t] + hpart[768 + t]);
       __syncthreads();
       EOI(6);  // 6: the update
-      derive();
       if (last_it) {  // the basis state for the host, the counters back at rest
-        __syncthreads();
+        const int KF = k * F;
         for (int e = t; e < KF; e += NT) a.H64[e] = sH64[e];
         for (int e = t; e < F * bm::KP; e += NT) {
           const int f = e / bm::KP, n = e - f * bm::KP;
@@ -2741,9 +2803,10 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         }
         return;
       }
+      put_terms([&](int n, int f) { return sH64[n * F + f]; });
       zero_pads();
       __syncthreads();
-      EOI(7);  // 7: H terms, HHᵀ, pads
+      EOI(7);  // 7: H terms, pads
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) hhb[kk] = sHHt[(4 * kk + g) * bm::KP + li];
 #pragma unroll
@@ -3404,6 +3467,14 @@ __device__ __forceinline__ float sum_over_samples(float v) {
   return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);  // + lane ^ 32
 }
 
+// v summed over the 16 lanes of its row (every lane gets the row's sum)
+__device__ __forceinline__ float sum_over_row16(float v) {
+  v += dppf<0x128>(v);  // row_ror:8
+  v += dppf<0x124>(v);  // row_ror:4
+  v += dppf<0x122>(v);  // row_ror:2
+  return v + dppf<0x121>(v);  // row_ror:1
+}
+
 // The X (and streamed W) prefetch lives in AGPRs and never touches a VGPR: inline-asm loads into
 // AGPR tuples, an asm wait naming them "+a", and asm ds_write_b128 straight from the AGPRs into
 // the staging slot (cdna_hip_programming.md §5.7 item 1, form ii).  Two reasons: (1) hipcc's own
@@ -3654,7 +3725,9 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, NACC = G_::NACC;
   constexpr int PFW = G_::PFW, LASTL = G_::LASTL;
   constexpr int PFS = PFW + (WRES ? 0 : 1);  // loads per prefetch set (+ the W tile when streamed)
-  constexpr int NSTB = (WRES ? 0 : 1) + (TOL ? 1 : 0);  // stores per body (W streamed; TOL's snapshot)
+  // stores per body: W streamed — its W tile, and TOL's snapshot of the checked state's W (a resident
+  // W keeps that snapshot in LDS: no store, so the counted waits are the plain kernel's)
+  constexpr int NSTB = (WRES ? 0 : 1) + (TOL && !WRES ? 1 : 0);
   constexpr int KP = KK / 2;                 // component pairs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
@@ -3692,6 +3765,10 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   float* wsnap = (TOL && !WRES)
                      ? reinterpret_cast<float*>(__double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP)))
                      : nullptr;
+  // TOL with W resident: the W of the state a loss iteration checks, this wave's tiles [i][TSW][K],
+  // after the four waves' resident W (the host sizes the LDS for both)
+  float* wsnapl = (TOL && WRES) ? reinterpret_cast<float*>(smem + G_::L_WRES + (size_t)(NWV + w) * nbt_max * WBW)
+                                : nullptr;
   double lossacc = 0.0;  // this lane's ‖x − w·H‖² over the iteration's tiles (loss iterations)
   uint32_t* cnt_group = a.cnt + CNT_GROUP0 + 32 * g;
   uint32_t* cnt_top = a.cnt + CNT_TOP;
@@ -3892,15 +3969,16 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     const float wold32 = wt_[s * KK + e];
     const double wold = (double)wold32;
-    if constexpr (TOL) {
-      // the W of the state a loss iteration checks, ONE store per body in every iteration (the
-      // steps' waits count it): a loss iteration stores the tile's W into W itself (resident W: HBM
-      // is not read again in this launch) or the snapshot buffer (streamed W); the others store the
-      // same value over the wave's first tile there, which the next loss iteration or the launch's
-      // write-back overwrites (a stop happens only at the end of a loss iteration)
+    if constexpr (TOL && WRES) {
+      // the W of the state a loss iteration checks, kept in LDS (written to HBM only on a stop)
+      if (loss_it) wsnapl[i * (TSW * KK) + s * KK + e] = wold32;
+    } else if constexpr (TOL) {
+      // W streamed: the W of the checked state, ONE store per body in every iteration (the steps'
+      // waits count it): a loss iteration stores the tile's W into the snapshot buffer, the others
+      // the same value over the wave's first tile there, which the next loss iteration overwrites
+      // (a stop happens only at the end of a loss iteration)
       const int64_t tsel = loss_it ? tile : (int64_t)gw;
-      float* snap = WRES ? reinterpret_cast<float*>(Wb) : wsnap;
-      snap[(size_t)tsel * TSW * KK + l] = wold32;
+      wsnap[(size_t)tsel * TSW * KK + l] = wold32;
     }
     if (loss_it) {
       // ‖x − w·H‖² of the state before this update, the lane's NQ features (the last lane's overrun
@@ -4078,9 +4156,16 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
     }
     if (TOL && sFlag[3]) {
-      // stopped by the tolerance test: the state after it0 + it iterations (W already where it
-      // belongs, H = sH not updated); the host clears the flag word after the launch
+      // stopped by the tolerance test: the state after it0 + it iterations (W: the loss
+      // iteration's LDS snapshot written back here, or the host copies the streamed-W snapshot
+      // buffer; H = sH not updated); the host clears the flag word after the launch
       alive = false;
+      if (WRES)
+        for (int c = l; c < nbt * (WBW / 16); c += 64) {
+          const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
+          *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
+              *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wsnapl) + ii * WBW + 16 * ch);
+        }
       if (!top) return;
       for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
       for (int o = t; o < F * KK; o += NT) {
@@ -5572,15 +5657,15 @@ static int64_t max_resident(PassFn fn, size_t lds) {
 
 // the persistent cfg4 launch (mu_iter_bfw_kernel): bf16 X, F with 10 K-steps (289..320), k = 16,
 // whole 64-sample tiles, >= 6 wave-tile pairs' worth of tiles per workgroup (the prefetch of the
-// next iteration's first pair must find its W' retired), the grid co-resident.  CNMF_BFW_PERSIST=0
-// (diagnostic build) keeps the per-iteration launches for A/B runs.
+// next iteration's first pair must find its W' retired), the grid co-resident.  Layout 6 only (the
+// per-iteration launches, layout 4, were faster on the MI355X measured: DESIGN §3.4).
 struct BwpLaunch {
   int64_t G, n_tiles;
   size_t lds;
 };
-static bool bwp_plan(int64_t n_rows, int x_dtype, int F, int k, BwpLaunch* out) {
+static bool bwp_plan(int64_t n_rows, int x_dtype, int F, int k, int layout, BwpLaunch* out) {
+  if (layout != 6) return false;  // opt-in: MUPlan.tune() times it against the per-iteration launches
   if (!use_bfw(x_dtype, F, k) || bm::ksteps(F) != 10 || k != 16 || n_rows <= 0 || n_rows % TS != 0) return false;
-  if (diag_env("CNMF_BFW_PERSIST") && atoi(diag_env("CNMF_BFW_PERSIST")) == 0) return false;
   const size_t lds = (size_t)bw::lds(F).total + align16((size_t)k * F * 8) + 16;
   if (lds > kMaxLds) return false;
   const int64_t n_tiles = n_rows / TS;
@@ -6603,8 +6688,16 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
 }
 
 // HREG (diagnostic A/B, one workgroup per CU): the lane's fp64 Hᵀ rows held in VGPRs for the
-// iteration instead of re-read from LDS every tile (42 ds_read_b128 per wave tile)
-template <int PD, int OCC, bool MULTI = false, bool HREG = false>
+// iteration instead of re-read from LDS every tile (42 ds_read_b128 per wave tile).
+// MF: phase 1 (c = H·x, fp64) on the matrix cores — 21 v_mfma_f64_4x4x4f64 per wave tile instead of
+// 84 fp64 FMAs, 42 ds_read_b128 of Hᵀ and the quad butterfly.  The instruction's operand layout
+// (profiles/r04/mfma_f64_layout.txt): A[b][i][k] at lane i + 4b + 16k, B[b][k][j] at lane
+// j + 4b + 16k, D[b][i][j] at lane 16i + 4b + j.  So with sample s = 4i + b the result c[s][j] lands
+// on lane 4s + j (the FCLS's quad layout) when lane L holds x of sample 4(L % 4) + (L / 4) % 4 and
+// feature group k = L / 16 (features 21k .. 21k + 20; B = H[j][21k + q] from VGPRs); phase 3 then
+// takes the sample's new row w' through the wave's LDS slot and its sums run over the 16 lanes of a
+// row (one feature group).  MFL: the B operand read from LDS per tile (ds_read_b64) instead of VGPRs.
+template <int PD, int OCC, bool MULTI = false, bool HREG = false, bool MF = false, bool MFL = false>
 __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
@@ -6617,6 +6710,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   const int l = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int s = l / NL, e = l % NL;
+  // the sample and feature group whose x this lane holds (phases 1 and 3): MF the matrix-core A layout
+  const int sx = MF ? 4 * (l & 3) + ((l >> 2) & 3) : s, ex = MF ? (l >> 4) : e;
   const int b = blockIdx.x;
   const int G = gridDim.x;
   const int NW = NWV * G;
@@ -6644,12 +6739,18 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   __syncthreads();
   wa_derive(smem, t, a.delta2);
   double hreg[HREG ? NQ : 1][KK];
+  double hb[MF ? NQ : 1];  // MF: the B operand H[e][21 ex + q] (Hᵀ rows >= F are zero)
+  const double* hbl = reinterpret_cast<const double*>(smem + wa::L_HT) + NQ * ex * KK + e;  // MFL: from LDS
   auto load_h = [&]() {
     if constexpr (HREG) {
 #pragma unroll
       for (int c = 0; c < NQ; ++c)
 #pragma unroll
         for (int j = 0; j < KK; ++j) hreg[c][j] = sHtl[c * KK + j];
+    }
+    if constexpr (MF && !MFL) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) hb[q] = hbl[q * KK];
     }
   };
   load_h();
@@ -6707,11 +6808,27 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   auto wbody = [&](int i) {
     const int64_t tile = gw + (int64_t)NW * i;
     // phase 1: c = H·x over the lane's features in fp64, quad butterfly, + δ²
-    const float* xr = reinterpret_cast<const float*>(stg) + s * wa::F + NQ * e;
+    const float* xr = reinterpret_cast<const float*>(stg) + sx * wa::F + NQ * ex;
     float xv[NQ];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) xv[c] = xr[c];
     double cc[KK] = {0.0, 0.0, 0.0, 0.0};
+    if constexpr (MF) {
+      // three accumulation chains (the MFMA's dependent latency), summed in a fixed order
+      double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+      auto hbq = [&](int q) { return MFL ? hbl[q * KK] : hb[MFL ? 0 : q]; };
+#pragma unroll
+      for (int q = 0; q < NQ; q += 3) {
+        m0 = __builtin_amdgcn_mfma_f64_4x4x4f64((double)xv[q], hbq(q), m0, 0, 0, 0);
+        if (q + 1 < NQ) m1 = __builtin_amdgcn_mfma_f64_4x4x4f64((double)xv[q + 1], hbq(q + 1), m1, 0, 0, 0);
+        if (q + 2 < NQ) m2 = __builtin_amdgcn_mfma_f64_4x4x4f64((double)xv[q + 2], hbq(q + 2), m2, 0, 0, 0);
+      }
+      const double cs = ((m0 + m1) + m2) + a.delta2;  // c[s][e] + δ² on lane 4s + e
+      cc[0] = dpp64<0x00>(cs);                         // quad broadcasts: lane 4s + j's value
+      cc[1] = dpp64<0x55>(cs);
+      cc[2] = dpp64<0xAA>(cs);
+      cc[3] = dpp64<0xFF>(cs);
+    } else {
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
       const double2 h01 = HREG ? make_double2(hreg[HREG ? c : 0][0], hreg[HREG ? c : 0][1])
@@ -6728,6 +6845,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     for (int j = 0; j < KK; ++j) cc[j] += dpp64<0xB1>(cc[j]);  // quad_perm [1,0,3,2]: + lane ^ 1
 #pragma unroll
     for (int j = 0; j < KK; ++j) cc[j] = cc[j] + dpp64<0x4E>(cc[j]) + a.delta2;  // [2,3,0,1]: + lane ^ 2
+    }
     // FCLS: the passive sets e, e + 4, e + 8, e + 12
     double bestf = 1.0;
     int bestm = 16;
@@ -6768,8 +6886,20 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
     const float wn = (float)fmax(wn64, 0.0);
     a.W[(size_t)tile * (16 * KK) + l] = wn;  // lane l = (s, e): the tile's 256 contiguous bytes
-    // phase 3 with the sample's new row (quad broadcasts)
-    const f2 wp[KP] = {f2{dppf<0x00>(wn), dppf<0x55>(wn)}, f2{dppf<0xAA>(wn), dppf<0xFF>(wn)}};
+    // phase 3 with the sample's new row: quad broadcasts, or (MF) the row of sample sx through the
+    // wave's staging slot (its X was read above: in-order LDS inside the wave)
+    f2 wp[KP];
+    float wk = wn;  // B[ex][·] += w'[ex]·w'
+    if constexpr (MF) {
+      reinterpret_cast<float*>(stg)[l] = wn;
+      const float4 wq = *reinterpret_cast<const float4*>(stg + 16 * sx);
+      wp[0] = f2{wq.x, wq.y};
+      wp[1] = f2{wq.z, wq.w};
+      wk = ex == 0 ? wq.x : (ex == 1 ? wq.y : (ex == 2 ? wq.z : wq.w));
+    } else {
+      wp[0] = f2{dppf<0x00>(wn), dppf<0x55>(wn)};
+      wp[1] = f2{dppf<0xAA>(wn), dppf<0xFF>(wn)};
+    }
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
       const f2 xx = f2{xv[c], xv[c]};
@@ -6777,22 +6907,23 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       for (int q = 0; q < KP; ++q) acc[c][q] = __builtin_elementwise_fma(xx, wp[q], acc[c][q]);
     }
 #pragma unroll
-    for (int q = 0; q < KP; ++q) accB[q] = __builtin_elementwise_fma(f2{wn, wn}, wp[q], accB[q]);
+    for (int q = 0; q < KP; ++q) accB[q] = __builtin_elementwise_fma(f2{wk, wk}, wp[q], accB[q]);
   };
   auto end_iteration = [&](int it) {
     const bool last_it = it + 1 == a.n_iter;
     // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
     {
-      float* rw = red + (w * NL + e) * NACC;
+      // the sums over the lanes of one feature group: lanes ≡ e (mod 4), or (MF) the 16 lanes of a row
+      auto ssum = [&](float v) { return MF ? sum_over_row16(v) : sum_over_samples<NL>(v); };
+      const bool wr = MF ? (l & 15) == 0 : l < NL;
+      float* rw = red + (w * NL + ex) * NACC;
 #pragma unroll
       for (int c = 0; c < NQ; ++c) {
-        const float4 v = make_float4(sum_over_samples<NL>(acc[c][0].x), sum_over_samples<NL>(acc[c][0].y),
-                                     sum_over_samples<NL>(acc[c][1].x), sum_over_samples<NL>(acc[c][1].y));
-        if (l < NL) *reinterpret_cast<float4*>(rw + c * KK) = v;
+        const float4 v = make_float4(ssum(acc[c][0].x), ssum(acc[c][0].y), ssum(acc[c][1].x), ssum(acc[c][1].y));
+        if (wr) *reinterpret_cast<float4*>(rw + c * KK) = v;
       }
-      const float4 v = make_float4(sum_over_samples<NL>(accB[0].x), sum_over_samples<NL>(accB[0].y),
-                                   sum_over_samples<NL>(accB[1].x), sum_over_samples<NL>(accB[1].y));
-      if (l < NL) *reinterpret_cast<float4*>(rw + NQ * KK) = v;
+      const float4 v = make_float4(ssum(accB[0].x), ssum(accB[0].y), ssum(accB[1].x), ssum(accB[1].y));
+      if (wr) *reinterpret_cast<float4*>(rw + NQ * KK) = v;
     }
     zero_acc();
     __syncthreads();
@@ -7393,17 +7524,17 @@ static int default_layout() {
 static int resolve_layout(int layout) {
   if (layout == 0) return default_layout();
 #ifdef CNMF_DIAG
-  return (layout >= 1 && layout <= 5) ? layout : -1;
+  return (layout >= 1 && layout <= 6) ? layout : -1;
 #else
-  return (layout == 4 || layout == 5) ? layout : -1;
+  return (layout >= 4 && layout <= 6) ? layout : -1;
 #endif
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
-      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 4 (wave tiles) or 5 (k = 8 wave tiles on "  \
-                     "the matrix cores); 1-3 are in the diagnostic build only");                          \
+      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 4 (wave tiles), 5 (k = 8 wave tiles on "   \
+                     "the matrix cores) or 6 (cfg4 persistent); 1-3 are in the diagnostic build only");   \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
 #ifndef CNMF_DIAG
@@ -7542,7 +7673,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
     if (G < 1) continue;
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
-    const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw : 0);
+    // W resident: the four waves' W tiles; TOL (the wave-tile kernel) a second copy: the snapshot of
+    // the checked state
+    const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw * (tol && !mf ? 2 : 1) : 0);
     if (lds > kMaxLds) continue;
     const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
@@ -7582,12 +7715,14 @@ struct WaLaunch {
 // workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2, default 2: two waves per SIMD hide the
 // fp64 and LDS latencies of the W-step, at 256 registers per lane and PD = 2; measured on one box,
 // cfg5: 146.6 us per iteration at 1, 123.1 us at 2, profiles/r02/session5/als_iter)
-// (diagnostic build: CNMF_ALS_OCC=1 one workgroup per CU, =3 one per CU with Hᵀ in VGPRs (HREG))
+// (diagnostic build: CNMF_ALS_OCC=1 one workgroup per CU, =3 one per CU with Hᵀ in VGPRs (HREG),
+// =4 two per CU with phase 1 on the matrix cores (MF), =5 one per CU with MF, =6 two per CU with
+// MF and its B operand from LDS (MFL))
 static int wa_variant() {
   static const int v = diag_env("CNMF_ALS_OCC") ? atoi(diag_env("CNMF_ALS_OCC")) : 2;
-  return (v == 1 || v == 3) ? v : 2;
+  return (v >= 1 && v <= 6) ? v : 2;
 }
-static int wa_occ() { return wa_variant() == 2 ? 2 : 1; }
+static int wa_occ() { return (wa_variant() == 2 || wa_variant() == 4 || wa_variant() == 6) ? 2 : 1; }
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
 static PassFn wa_fn(bool multi = false) {
 #ifdef CNMF_DIAG
@@ -7597,6 +7732,15 @@ static PassFn wa_fn(bool multi = false) {
   if (wa_variant() == 3)
     return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true, true>)
                  : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, false, true>);
+  if (wa_variant() == 4)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, true>);
+  if (wa_variant() == 5)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true, false, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, false, false, true>);
+  if (wa_variant() == 6)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, true, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, true, true>);
 #endif
   return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>)
                : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
@@ -7721,7 +7865,7 @@ int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dty
   if (wt_plan(n_rows, x_dtype, n_features, k, (multi & 1) != 0, layout, &L, (multi & 2) != 0)) return L.G;
   if (multi & 2) return 0;  // cnmf_mu_fit_tol serves the wave tiles only
   BwpLaunch B;
-  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) return (multi & 1) ? 0 : B.G;  // cfg4: one GPU only
+  if (bwp_plan(n_rows, x_dtype, n_features, k, layout, &B)) return (multi & 1) ? 0 : B.G;  // cfg4: one GPU only
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k, (multi & 1) != 0);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : g;
 }
@@ -7729,8 +7873,6 @@ int64_t cnmf_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dty
 int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   WtLaunch L;
   if (wt_plan(n_rows, x_dtype, n_features, k, false, 4, &L)) return 1;
-  BwpLaunch B;
-  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) return 1;
   const int64_t g = persist_grid(n_rows, x_dtype, n_features, k);
   return g < 0 ? set_err(CNMF_ERR_HIP, "occupancy query failed") : (g > 0 ? 1 : 0);
 }
@@ -7756,7 +7898,7 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
     return 1;
   }
   BwpLaunch B;
-  if (bwp_plan(n_rows, x_dtype, n_features, k, &B)) {
+  if (bwp_plan(n_rows, x_dtype, n_features, k, layout, &B)) {
     snprintf(out, (size_t)len,
              "mu_iter_bfw_kernel<k=16, F=%d>: bf16 matrix-core wave tiles, one 4-wave workgroup per CU (%lld "
              "workgroups), reduction and basis update in the launch",
@@ -8042,7 +8184,7 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
   }
   {  // cfg4: the bf16 wave-tile pass with the reduction and the basis update in the launch
     BwpLaunch B;
-    if (bwp_plan(n_rows, x_dtype, n_features, k, &B) && B.G <= n_parts) {
+    if (bwp_plan(n_rows, x_dtype, n_features, k, layout, &B) && B.G <= n_parts) {
       if (!X || !W || !H64 || !Ht || !HHt || !partials || !counter || !AB)
         return set_err(CNMF_ERR_ARG, "null pointer argument");
       if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))

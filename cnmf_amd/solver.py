@@ -136,6 +136,16 @@ class MUPlan:
         with torch.cuda.device(self.device):
             xg = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, 0, 1) if self.persistent_shape else 0
         self.exchange_shape = self.persistent_shape and int(xg) > 0
+        # the persistent layouts tune() chooses between for this shape (include/cnmf_hip.h `layout`):
+        # k = 8 fp32: the VALU (4) or matrix-core (5) wave tiles; cfg4's bf16 shape: the per-iteration
+        # launches (4) or ONE persistent launch (6)
+        self.layouts = ()
+        if self.persistent_shape and self.k == 8 and self.xdt == _lib.F32:
+            self.layouts = (4, 5)
+        elif self.xdt == _lib.BF16 and self.world == 1 and not self.persistent_shape:
+            with torch.cuda.device(self.device):
+                if int(self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, 6, 0)) > 0:
+                    self.layouts = (4, 6)
         self.persistent = self.persistent_shape and self.world == 1  # ...as one multi-iteration launch
         self.layout = 0  # layout of the persistent launch (include/cnmf_hip.h; 0 = default); tune() sets it
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
@@ -279,6 +289,8 @@ class MUPlan:
         single rank — a diagnostic of that path's per-iteration cost."""
         self.shard_steps = True
         self.persistent = False
+        if 6 in getattr(self, "layouts", ()):
+            self.set_layout(4)
 
     # -- plumbing ------------------------------------------------------------------------------
     def _stream(self):
@@ -448,11 +460,9 @@ class MUPlan:
         partial sums).  Call after the GPU has been busy for a while (the clock ramps up over the
         first ~35 ms of work).  Returns {layout: µs per iteration, the slowest rank's}.  No-op
         (empty dict) for non-persistent plans."""
-        if not self.persistent or self.k not in (4, 8) or self.xdt != _lib.F32:
-            return {}  # the layouts are alternatives for fp32 k = 4 and k = 8 only
-        if variants is None:  # k = 8: the VALU wave tiles (4) or the matrix-core wave tiles (5)
-            variants = (4, 5) if self.k == 8 else (4,)
-        if len(variants) < 2:
+        if variants is None:
+            variants = self.layouts
+        if len(variants) < 2 or (self.world > 1 and not self.persistent):
             return {}
         W0, H0 = self.W.clone(), self.H64.clone()
         keep = self.layout
@@ -460,17 +470,24 @@ class MUPlan:
         try:
             for _ in range(rounds):
                 for v in variants:
-                    self.layout = v
+                    self.set_layout(v)
                     times[v].append(self._time_iterations(n_iter) * 1e6 / n_iter)
         finally:
             self.W.copy_(W0)
             self.H64.copy_(H0)
             self.refresh_basis()
-            self.layout = keep
+            self.set_layout(keep)
         mean = [sum(times[v]) / len(times[v]) for v in variants]
         mean = dict(zip(variants, agree_max(mean, self.group if self.world > 1 else None, self.device)))
-        self.layout = min(variants, key=lambda v: (mean[v], variants.index(v)))
+        self.set_layout(min(variants, key=lambda v: (mean[v], variants.index(v))))
         return mean
+
+    def set_layout(self, layout: int):
+        """The persistent layout of this plan's launches; layout 6 (cfg4's shape) makes the plan a
+        one-launch persistent one, layout 4 there keeps the per-iteration launches."""
+        self.layout = int(layout)
+        if 6 in getattr(self, "layouts", ()):
+            self.persistent = self.layout == 6
 
     def _time_iterations(self, n_iter: int) -> float:
         """Seconds of one n_iter launch on the plan's stream (HIP events); raises on a failed launch."""
@@ -624,6 +641,8 @@ def _iterate_guarded(plan, n_iter: int, update_H: bool):
             plan.disable_exchange()
         plan.exchange = False
         plan.persistent = False
+        if 6 in getattr(plan, "layouts", ()):  # cfg4's persistent layout: back to its launches
+            plan.set_layout(4)
         plan.iterate(n_iter, update_H)
         plan.check_sync_error()
 
@@ -647,6 +666,8 @@ def _run_mu_device_tol(plan, max_iter, tol, verbose, return_errors):
             plan.disable_exchange()
         plan.exchange = False
         plan.persistent = False
+        if 6 in getattr(plan, "layouts", ()):
+            plan.set_layout(4)
         return None
     n_iter, errors = res
     if (verbose or return_errors) and n_iter == max_iter and max_iter % 10 == 0:

@@ -113,8 +113,11 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *       8-sample (k = 8) tiles with no barrier inside an iteration, W resident in LDS when it fits;
  *   5 = k = 8 only: the wave tiles with both products on the matrix cores (v_mfma_f32_16x16x4_f32,
  *       16-sample tiles; n_rows a multiple of 16, else layout 4);
- * MUPlan.tune() times 4 and 5 at k = 8 and keeps the faster for its plan; other values are
- * CNMF_ERR_ARG.  (Layouts 1-3, the round-1 workgroup-tile kernel, exist in the diagnostic build
+ *   6 = bf16 X, F = 289..320, k = 16, n_rows a multiple of 64 (cfg4): n iterations as ONE launch of
+ *       mu_iter_bfw_kernel (the pass, the reduction and the basis update in the launch; one GPU);
+ *       layout 4 is that shape's per-iteration launches;
+ * MUPlan.tune() times 4 and 5 at k = 8 (4 and 6 for cfg4's shape) and keeps the faster for its
+ * plan; other values are CNMF_ERR_ARG.  (Layouts 1-3, the round-1 workgroup-tile kernel, exist in the diagnostic build
  * only: DESIGN §3.0b.) */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
@@ -125,9 +128,8 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *   persistent: events[0] / events[1] before / after the launch (n_events >= 2);
  *   otherwise : events[2i] / events[2i+1] around iteration i: its pass, reduction and basis
  *               update (n_events >= 2*n_iter).
- * Persistent shapes: fp32 F = 81, k = 4 / 8 (mu_iter_wt_kernel) and bf16 F = 289..320, k = 16
- * with n_rows a multiple of 64 (mu_iter_bfw_kernel, cfg4: the reduction and the update inside the
- * launch too). */
+ * Persistent shapes: fp32 F = 81, k = 4 / 8 (mu_iter_wt_kernel), and with layout 6 bf16
+ * F = 289..320, k = 16, n_rows a multiple of 64 (mu_iter_bfw_kernel, cfg4). */
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,
                        double* HHt, double* partials, int64_t n_parts, double* stage,
                        uint32_t* counter, double* AB, double* stats, int64_t n_rows,

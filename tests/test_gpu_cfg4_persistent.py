@@ -1,4 +1,4 @@
-"""cfg4 (bf16 X, F = 300, k = 16) as ONE persistent launch (mu_iter_bfw_kernel):
+"""cfg4 (bf16 X, F = 300, k = 16) as ONE persistent launch (mu_iter_bfw_kernel, layout 6):
 the bf16 wave-tile pass with the cross-workgroup reduction (a reduce-scatter between two grid
 barriers) and the basis update (SK:634-728, fp64, every workgroup on its own LDS copy) inside the
 launch.
@@ -28,10 +28,14 @@ def _data(n, seed):
     return Xb, Xr, W0, H0
 
 
-def _plan(Xb, W0, H0, **regs):
+def _plan(Xb, W0, H0, layout=6, **regs):
+    """layout 6: the persistent launch (opt-in; MUPlan.tune() times it against layout 4, the
+    per-iteration launches)."""
     import torch
     from cnmf_amd.solver import MUPlan
     plan = MUPlan(Xb.cuda(), 16, **regs)
+    assert plan.layouts == (4, 6), plan.layouts
+    plan.set_layout(layout)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(torch.from_numpy(H0))
     return plan
@@ -65,12 +69,11 @@ def test_persistent_cfg4_500_iterations_matches_oracle():
 def test_persistent_agrees_with_launches_and_splits(n_tiles):
     import torch
     Xb, Xr, W0, H0 = _data(64 * n_tiles, n_tiles)
-    a, b, c = _plan(Xb, W0, H0), _plan(Xb, W0, H0), _plan(Xb, W0, H0)
-    assert a.persistent
+    a, b, c = _plan(Xb, W0, H0), _plan(Xb, W0, H0), _plan(Xb, W0, H0, layout=4)
+    assert a.persistent and not c.persistent  # c: the per-iteration launches (pass + reduce + update)
     a.iterate(40)
     for n in (1, 9, 30):
         b.iterate(n)
-    c.persistent = False  # the per-iteration launches (pass + reduce + split basis update)
     c.iterate(40)
     torch.cuda.synchronize()
     for p in (a, b):
@@ -121,6 +124,7 @@ def test_failed_persistent_cfg4_launch_falls_back():
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
     plan2 = _plan(Xb, W0, H0)
     n2 = run_mu(plan2, max_iter=300, tol=1e-3)
+    assert plan2.persistent
     _, _, nr = mu_ref.mu_fit(Xr.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
                              max_iter=300, tol=1e-3)
     assert n2 == nr

@@ -13,8 +13,8 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-NAMES = ["", "waves' sums -> partial row", "barrier A", "reduce-scatter", "barrier B", "AB -> LDS",
-         "basis update", "H terms + HHt + pads"]
+NAMES = ["", "waves' sums -> partial row (stores issued)", "barrier A", "reduce-scatter", "barrier B",
+         "AB -> LDS", "basis update + HHt (f64 MFMA)", "H terms + pads", "partial row stores retired"]
 
 
 def main():
@@ -47,7 +47,7 @@ def main():
     fn(buf, 1)
     pairs = max(buf[15], 1)
     out = {"us_per_iteration": round(us, 2), "wg_iterations": int(pairs)}
-    for i in range(1, 8):
+    for i in range(1, 9):
         out[NAMES[i]] = round(buf[i] / pairs, 1)
     print(json.dumps(out), flush=True)
 

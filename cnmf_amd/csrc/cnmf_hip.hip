@@ -4838,6 +4838,7 @@ __device__ double als_L_entry(int F, int a, int b) {  // (DᵀD)[a][b], b >= a, 
 #ifdef CNMF_STAMPS
 // diagnostic: per H-step call of workgroup 0 (the first 64 calls) and row: BPP iterations, cycles
 __device__ unsigned long long g_hs[64 * 4 * 2];
+__device__ unsigned long long g_hsp[64 * 4 * 4];  // wave H-step: [call][row][setup, gather, PCR, check] cycles
 __device__ unsigned int g_hs_calls;
 #endif
 __device__ __forceinline__ void als_hstep_block(unsigned char* smem, int F, int k, double lam, int t) {
@@ -5052,13 +5053,15 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     int* idx = reinterpret_cast<int*>(vz + F) + 2 * F;
     const uint64_t lt = (1ull << lane) - 1ull;
     // λ·(DᵀD) entries of the lane's two features: the same for every row of the sweep
-    double ld0[2], le1[2], le2[2];
+    double ld0[2], le1[2], le2[2], lm1[2], lm2[2];  // lm1/lm2: λ·L[f-1][f], λ·L[f-2][f]
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int f = lane + 64 * c;
       ld0[c] = f < F ? lam * als_L_entry(F, f, f) : 0.0;
       le1[c] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
       le2[c] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
+      lm1[c] = (f < F && f >= 1) ? lam * als_L_entry(F, f - 1, f) : 0.0;
+      lm2[c] = (f < F && f >= 2) ? lam * als_L_entry(F, f - 2, f) : 0.0;
     }
     for (int j = 0; j < k; ++j) {
       const double bjj = sB[j * k + j];
@@ -5066,6 +5069,15 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #ifdef CNMF_STAMPS
       const unsigned long long hs_t0 = __builtin_amdgcn_s_memtime();
       int hs_iters = 0;
+      unsigned long long hs_ph[4] = {0, 0, 0, 0}, hs_m = hs_t0;
+      auto hs_mark = [&](int ph) {
+        const unsigned long long now = __builtin_amdgcn_s_memtime();
+        hs_ph[ph] += now - hs_m;
+        hs_m = now;
+      };
+#define HS_MARK(p) hs_mark(p)
+#else
+#define HS_MARK(p) ((void)0)
 #endif
       double rb[2], rd[2], re1[2], re2[2], xf[2];
       bool pas[2];
@@ -5090,7 +5102,54 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
         }
       }
       int alpha = 3, beta = F + 1;  // BPP control (wave-uniform)
+      // Jacobi: the row's Hessian M = B_jj·I + λ·DᵀD has off-diagonal row sums at most 10λ (the
+      // |1, −4, −4, 1| of DᵀD) against a diagonal >= B_jj, so ρ = 10λ / B_jj bounds the Jacobi
+      // contraction of any passive subsystem M_PP in the max norm.  At ρ <= 1/20 (B_jj is a sum over
+      // all samples: ρ ~ 1e-4 at cfg5) sweeps from the warm start x = h_j reach the fp64 fixed
+      // point in a few steps (bound: ρ^nsw <= 2^-55, and a sweep that changes no bit ends early) —
+      // the same solve as the block PCR below at a fraction of its per-row cost (two LDS round trips
+      // per sweep instead of six shuffle steps of 2x2 blocks and the passive-set compression).
+      const double rho = 10.0 * lam / bjj;
+      const bool jac = rho <= 0.05;
+      int nsw = 0;
+      for (double r = 1.0; jac && r > 0x1p-55; r *= rho) ++nsw;
+      double rinv[2] = {1.0 / rd[0], 1.0 / rd[1]};
+#pragma unroll
+      for (int c = 0; c < 2; ++c) xf[c] = pas[c] ? sH[j * F + lane + 64 * c] : 0.0;  // warm start
+      HS_MARK(0);
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
+       if (jac) {
+        // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P)
+        for (int sw = 0; sw < nsw; ++sw) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c)
+            if (lane + 64 * c < F) vx[lane + 64 * c] = xf[c];
+          lds_order();
+          bool chg = false;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int f = lane + 64 * c;
+            double xn = 0.0;
+            if (f < F && pas[c]) {
+              double r = rb[c];
+              if (f >= 1) r = fma(-lm1[c], vx[f - 1], r);
+              if (f + 1 < F) r = fma(-re1[c], vx[f + 1], r);
+              if (f >= 2) r = fma(-lm2[c], vx[f - 2], r);
+              if (f + 2 < F) r = fma(-re2[c], vx[f + 2], r);
+              xn = r * rinv[c];
+            }
+            chg = chg || xn != xf[c];
+            xf[c] = xn;
+          }
+          lds_order();
+          if (!__ballot(chg)) break;
+        }
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          if (lane + 64 * c < F) vx[lane + 64 * c] = xf[c];
+        lds_order();
+        HS_MARK(2);
+       } else {
         // ---- compress the passive set: idx[pos] = feature
         const uint64_t bal0 = __ballot(pas[0]), bal1 = __ballot(pas[1]);
         const int n0 = __popcll(bal0), n = n0 + __popcll(bal1);
@@ -5126,6 +5185,10 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           double b00 = p0m0, b01 = p1m1, b11 = p1m0;
           double a00 = p0m2, a01 = p0m1, a10 = 0.0, a11 = p1m2;
           double r0 = p0z, r1 = p1z;
+#ifdef CNMF_STAMPS
+          if (b00 + b11 + a00 + a11 + r0 + r1 == 12345.678) vb[0] = 0.0;  // the gathered entries landed
+#endif
+          HS_MARK(1);
           auto inv2 = [](double x00, double x01, double x11, double& i00, double& i01, double& i11) {
             const double det = fmax(fma(x00, x11, -x01 * x01), 1e-300);
             double id = __builtin_amdgcn_rcp(det);
@@ -5169,6 +5232,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           if (2 * lane + 1 < n) vz[2 * lane + 1] = fma(i01, r0, i11 * r1);
         }
         lds_order();
+        HS_MARK(2);
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           const int f = lane + 64 * c;
@@ -5176,6 +5240,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           if (f < F) vx[f] = xf[c];
         }
         lds_order();
+       }
         bool bad[2];
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
@@ -5206,11 +5271,13 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #ifdef CNMF_STAMPS
         ++hs_iters;
 #endif
+        HS_MARK(3);
         if (mode == 0) break;
 #pragma unroll
         for (int c = 0; c < 2; ++c)
           if ((mode == 1 && bad[c]) || (mode == 2 && lane + 64 * c == maxbad)) pas[c] = !pas[c];
       }
+#undef HS_MARK
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         if (lane + 64 * c < F) sH[j * F + lane + 64 * c] = fmax(xf[c], 0.0);
@@ -5219,6 +5286,8 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       if (lane == 0 && hs_call < 64u && j < 4) {
         g_hs[(hs_call * 4 + j) * 2] = (unsigned long long)hs_iters;
         g_hs[(hs_call * 4 + j) * 2 + 1] = __builtin_amdgcn_s_memtime() - hs_t0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g_hsp[(hs_call * 4 + j) * 4 + q] = hs_ph[q];
       }
 #endif
     }
@@ -6638,6 +6707,7 @@ struct AlsPersistArgs {
   double delta2;     // sum_to_one²
   double lam;        // smoothness
   uint64_t* xctl;    // MULTI: the cross-rank exchange control block (mu_iter_wt_kernel's protocol)
+  int prio;          // diag (CNMF_ALS_PRIO): the issue-priority ladder over an iteration's steps
 };
 
 // Hᵀ (fp64, the lanes' feature blocks), HHᵀ (fp64; 16 threads per entry, fixed xor tree) and the
@@ -6697,7 +6767,21 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
 // feature group k = L / 16 (features 21k .. 21k + 20; B = H[j][21k + q] from VGPRs); phase 3 then
 // takes the sample's new row w' through the wave's LDS slot and its sums run over the 16 lanes of a
 // row (one feature group).  MFL: the B operand read from LDS per tile (ds_read_b64) instead of VGPRs.
-template <int PD, int OCC, bool MULTI = false, bool HREG = false, bool MF = false, bool MFL = false>
+// MX: the whole W-step on the matrix cores (fp64), lane l = (sample s = l % 16, residue g = l / 16):
+//   phase 1  c[q][s] = Σ_f H[q][f]·x[s][f] on 21 v_mfma_f64_4x4x4f64 with A = H[q = l % 4][4ks + g]
+//            and B = x[s][4ks + g] (the lane's features are f ≡ g mod 4), so D lands on lane 16q + s:
+//            lane (s, g) holds c[g][s] — exactly the B operand of
+//   FCLS     four v_mfma_f64_16x16x4f64 (K = the 4 components): block b' evaluates the masks 4b' + i % 4
+//            for all 16 samples, A row i = (mask 4b' + i % 4, component r = (i / 4) ^ (i % 4)) of the
+//            table; the f64 16x16 D layout (row g + 4·reg on lane s + 16g) leaves on lane (s, g) the
+//            whole solution vector of mask 4b' + g, rotated: register ρ = component ρ ^ g.  With c
+//            rotated the same way (c[g ^ ρ] from lanes l ^ 16ρ by permlane swaps) the objective
+//            −½ c·v, the feasibility test and the choice (least objective, ties the lowest mask) are
+//            per-lane register work plus two swap rounds; w[s][g] = max(T_best[g]·c, 0) from the table.
+//   phase 3  A[g ^ ρ][4ks + g] += x·w[s][g ^ ρ], B[g][g ^ ρ] += w[s][g]·w[s][g ^ ρ] (rotated, fp32 per
+//            lane); the end of the iteration sums the 16 lanes of a row and un-rotates into the
+//            reduction's layout.
+template <int PD, int OCC, bool MULTI = false, bool HREG = false, bool MF = false, bool MFL = false, bool MX = false>
 __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
@@ -6741,7 +6825,27 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   double hreg[HREG ? NQ : 1][KK];
   double hb[MF ? NQ : 1];  // MF: the B operand H[e][21 ex + q] (Hᵀ rows >= F are zero)
   const double* hbl = reinterpret_cast<const double*>(smem + wa::L_HT) + NQ * ex * KK + e;  // MFL: from LDS
+  // MX: lane (sm, gm); the phase-1 A operand H[l % 4][4ks + gm] (registers at one workgroup per CU,
+  // else LDS per tile), the FCLS A operands (table rows) and the validity of the lane's four masks
+  const int sm = l & 15, gm = l >> 4;
+  constexpr bool MXR = MX && OCC == 1;
+  double hx[MXR ? NQ : 1];
+  const double* hxl = reinterpret_cast<const double*>(smem + wa::L_HT) + 4 * gm + (l & 3);  // + 16·ks
+  double tx[MX ? 4 : 1];
+  bool vx[MX ? 4 : 1];
   auto load_h = [&]() {
+    if constexpr (MX) {
+      if constexpr (MXR) {
+#pragma unroll
+        for (int ks = 0; ks < NQ; ++ks) hx[ks] = hxl[16 * ks];
+      }
+#pragma unroll
+      for (int bp = 0; bp < 4; ++bp) {
+        const int i = l & 15;
+        tx[bp] = sTab[(4 * bp + (i & 3)) * wa::TSTR + (((i >> 2) ^ (i & 3)) << 2) + gm];
+        vx[bp] = sTab[16 * wa::TSTR + 4 * bp + gm] != 0.0;
+      }
+    }
     if constexpr (HREG) {
 #pragma unroll
       for (int c = 0; c < NQ; ++c)
@@ -6805,7 +6909,86 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     prefetch(pfk, gw + (int64_t)NW * (nx_i < nbt ? nx_i : 0));
     if (++nx_i == nbp) nx_i = 0;
   };
+  // MX: the identity block — A row i = (g = i % 4, component (i / 4) ^ (i % 4)) of I — turns c[g][s]
+  // into the rotated copies c[g ^ ρ][s] in the D registers (exact: one product by 1, three zeros)
+  const double tid = ((((l & 15) >> 2) ^ (l & 3)) == gm) ? 1.0 : 0.0;
+  auto wbody_mx = [&](int i) {
+    const int64_t tile = gw + (int64_t)NW * i;
+    // phase 1: c[g][s] on lane (s, g); three accumulation chains summed in a fixed order
+    const float* xr = reinterpret_cast<const float*>(stg) + sm * wa::F + gm;
+    float xv[NQ];
+#pragma unroll
+    for (int ks = 0; ks < NQ; ++ks) xv[ks] = xr[4 * ks];
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0;
+    auto hq = [&](int ks) { return MXR ? hx[MXR ? ks : 0] : hxl[16 * ks]; };
+#pragma unroll
+    for (int ks = 0; ks < NQ; ks += 3) {
+      m0 = __builtin_amdgcn_mfma_f64_4x4x4f64(hq(ks), (double)xv[ks], m0, 0, 0, 0);
+      if (ks + 1 < NQ) m1 = __builtin_amdgcn_mfma_f64_4x4x4f64(hq(ks + 1), (double)xv[ks + 1], m1, 0, 0, 0);
+      if (ks + 2 < NQ) m2 = __builtin_amdgcn_mfma_f64_4x4x4f64(hq(ks + 2), (double)xv[ks + 2], m2, 0, 0, 0);
+    }
+    const double cs = ((m0 + m1) + m2) + a.delta2;  // c[gm][sm] + δ²
+    // c rotated: cr[ρ] = c[gm ^ ρ][sm]
+    const f64x4 cr = __builtin_amdgcn_mfma_f64_16x16x4f64(tid, cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+    // FCLS: the 16 masks' solutions, lane (s, g) block b' = mask 4b' + g (register ρ = component ρ ^ g);
+    // the lane's masks ascend with b', so a strict < keeps the lowest of tied masks
+    double bestf = 1.0;
+    int bestm = 16;
+#pragma unroll
+    for (int bp = 0; bp < 4; ++bp) {
+      const f64x4 v = __builtin_amdgcn_mfma_f64_16x16x4f64(tx[bp], cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+      const bool feas = vx[bp] & (v[0] >= 0.0) & (v[1] >= 0.0) & (v[2] >= 0.0) & (v[3] >= 0.0);
+      const double f = -0.5 * fma(cr[3], v[3], fma(cr[2], v[2], fma(cr[1], v[1], cr[0] * v[0])));
+      const bool take = feas & (f < bestf);
+      bestf = take ? f : bestf;
+      bestm = take ? 4 * bp + gm : bestm;
+    }
+    // the sample's four lanes exchange their best through the wave's staging slot (its x is in
+    // registers; in-order LDS inside the wave) and each takes the least (objective, mask)
+    double* xf_ = reinterpret_cast<double*>(stg);
+    int* xm_ = reinterpret_cast<int*>(stg + 512);
+    float* xw_ = reinterpret_cast<float*>(stg + 768);
+    xf_[4 * sm + gm] = bestf;
+    xm_[4 * sm + gm] = bestm;
+    {
+      const double4 fo = *reinterpret_cast<const double4*>(xf_ + 4 * sm);
+      const int4 mo = *reinterpret_cast<const int4*>(xm_ + 4 * sm);
+      auto pick = [&](double f2_, int m2_) {
+        const bool tk = (f2_ < bestf) | ((f2_ == bestf) & (m2_ < bestm));
+        bestf = tk ? f2_ : bestf;
+        bestm = tk ? m2_ : bestm;
+      };
+      bestf = fo.x;
+      bestm = mo.x;
+      pick(fo.y, mo.y);
+      pick(fo.z, mo.z);
+      pick(fo.w, mo.w);
+    }
+    double wn64;
+    {
+      const double* T = sTab + min(bestm, 15) * wa::TSTR + 4 * gm;
+      wn64 = fma(T[gm ^ 3], cr[3], fma(T[gm ^ 2], cr[2], fma(T[gm ^ 1], cr[1], T[gm] * cr[0])));
+    }
+    const float wn = (float)fmax(wn64, 0.0);
+    a.W[(size_t)tile * (16 * KK) + 4 * sm + gm] = wn;  // the tile's 256 contiguous bytes
+    // phase 3 with the sample's new row (through the slot)
+    xw_[4 * sm + gm] = wn;
+    const float4 w4 = *reinterpret_cast<const float4*>(xw_ + 4 * sm);
+    const f2 wp0 = f2{w4.x, w4.y}, wp1 = f2{w4.z, w4.w};
+#pragma unroll
+    for (int ks = 0; ks < NQ; ++ks) {
+      const f2 xx = f2{xv[ks], xv[ks]};
+      acc[ks][0] = __builtin_elementwise_fma(xx, wp0, acc[ks][0]);
+      acc[ks][1] = __builtin_elementwise_fma(xx, wp1, acc[ks][1]);
+    }
+    accB[0] = __builtin_elementwise_fma(f2{wn, wn}, wp0, accB[0]);
+    accB[1] = __builtin_elementwise_fma(f2{wn, wn}, wp1, accB[1]);
+  };
   auto wbody = [&](int i) {
+    if constexpr (MX) {
+      wbody_mx(i);
+      return;
+    }
     const int64_t tile = gw + (int64_t)NW * i;
     // phase 1: c = H·x over the lane's features in fp64, quad butterfly, + δ²
     const float* xr = reinterpret_cast<const float*>(stg) + sx * wa::F + NQ * ex;
@@ -6912,7 +7095,23 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   auto end_iteration = [&](int it) {
     const bool last_it = it + 1 == a.n_iter;
     // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
-    {
+    if constexpr (MX) {
+      // the 16 sample lanes of row g summed; the row's first lane writes features 4ks + g
+      const bool wr = sm == 0;
+#pragma unroll
+      for (int ks = 0; ks < NQ; ++ks) {
+        const float4 v = make_float4(sum_over_row16(acc[ks][0].x), sum_over_row16(acc[ks][0].y),
+                                     sum_over_row16(acc[ks][1].x), sum_over_row16(acc[ks][1].y));
+        const int f = 4 * ks + gm;
+        if (wr && f < wa::F) {
+          const int ee = f / NQ;
+          *reinterpret_cast<float4*>(red + (w * NL + ee) * NACC + (f - NQ * ee) * KK) = v;
+        }
+      }
+      const float4 v = make_float4(sum_over_row16(accB[0].x), sum_over_row16(accB[0].y),
+                                   sum_over_row16(accB[1].x), sum_over_row16(accB[1].y));
+      if (wr) *reinterpret_cast<float4*>(red + (w * NL + gm) * NACC + NQ * KK) = v;
+    } else {
       // the sums over the lanes of one feature group: lanes ≡ e (mod 4), or (MF) the 16 lanes of a row
       auto ssum = [&](float v) { return MF ? sum_over_row16(v) : sum_over_samples<NL>(v); };
       const bool wr = MF ? (l & 15) == 0 : l < NL;
@@ -7023,6 +7222,16 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
 
   for (int it = 0; it < a.n_iter && alive; ++it) {
     for (int i0 = 0; i0 < nbp; i0 += PD) {
+      if (a.prio) {
+        // the ladder: a wave with more steps left issues first, so the two workgroups sharing a CU
+        // (each SIMD runs one wave of each) finish their iteration together instead of the older one
+        // first and the younger alone at one wave per SIMD
+        const int rem = nbp - i0;
+        if (rem > 3 * a.prio) __builtin_amdgcn_s_setprio(3);
+        else if (rem > 2 * a.prio) __builtin_amdgcn_s_setprio(2);
+        else if (rem > a.prio) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
 #pragma unroll
       for (int k = 0; k < PD; ++k) {
         step(pf[k]);
@@ -7421,6 +7630,10 @@ int cnmf_debug_hstep(unsigned long long* host_out) {  // [64 calls][4 rows][BPP 
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hs), sizeof(unsigned long long) * 64 * 4 * 2));
   return CNMF_OK;
 }
+int cnmf_debug_hstep_phases(unsigned long long* host_out) {  // [64 calls][4 rows][4 phases] cycles
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hsp), sizeof(unsigned long long) * 64 * 4 * 4));
+  return CNMF_OK;
+}
 int cnmf_debug_xtimeline(unsigned long long* host_out) {
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_x), sizeof(unsigned long long) * TL_IT * 4));
   return CNMF_OK;
@@ -7720,9 +7933,12 @@ struct WaLaunch {
 // MF and its B operand from LDS (MFL))
 static int wa_variant() {
   static const int v = diag_env("CNMF_ALS_OCC") ? atoi(diag_env("CNMF_ALS_OCC")) : 2;
-  return (v >= 1 && v <= 6) ? v : 2;
+  return (v >= 1 && v <= 8) ? v : 2;
 }
-static int wa_occ() { return (wa_variant() == 2 || wa_variant() == 4 || wa_variant() == 6) ? 2 : 1; }
+static int wa_occ() {
+  const int v = wa_variant();
+  return (v == 2 || v == 4 || v == 6 || v == 7) ? 2 : 1;
+}
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
 static PassFn wa_fn(bool multi = false) {
 #ifdef CNMF_DIAG
@@ -7741,6 +7957,12 @@ static PassFn wa_fn(bool multi = false) {
   if (wa_variant() == 6)
     return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, true, true>)
                  : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, true, true>);
+  if (wa_variant() == 7)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, false, false, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, false, false, true>);
+  if (wa_variant() == 8)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true, false, false, false, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, false, false, false, false, true>);
 #endif
   return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>)
                : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
@@ -7800,6 +8022,7 @@ static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, doubl
   pa.delta2 = sum_to_one * sum_to_one;
   pa.lam = smoothness;
   pa.xctl = xctl;
+  pa.prio = diag_env("CNMF_ALS_PRIO") ? atoi(diag_env("CNMF_ALS_PRIO")) : 0;  // steps per ladder band
   void* args[] = {&pa};
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn(multi)), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));

@@ -68,14 +68,18 @@ def test_w_step_matches_scipy_nnls(F, k, delta):
     np.testing.assert_allclose(AB[:, F:], Wg.T @ Wg, rtol=2e-6)
 
 
-@pytest.mark.parametrize("F", [17, 81, 128, 129, 300])  # <= 128: one-wave PCR form; above: workgroup LDLᵀ
+# F <= 128: the one-wave form (Jacobi sweeps when 10λ <= B_jj / 20, else the block PCR); above: the
+# workgroup LDLᵀ.  scale = 500: the accumulators of 500x the samples (1e6 rows, cfg5's B_jj), where
+# the one-wave form takes the Jacobi sweeps even at λ = 20; at scale 1 (2000 rows) λ = 20 takes the PCR
+@pytest.mark.parametrize("F", [17, 81, 128, 129, 300])
 @pytest.mark.parametrize("lam", [0.0, 0.5, 20.0])
-def test_h_step_matches_scipy_nnls(F, lam):
+@pytest.mark.parametrize("scale", [1.0, 500.0])
+def test_h_step_matches_scipy_nnls(F, lam, scale):
     import torch
     k = 4
     X, W0, H0 = _data(2000, F, k, seed=3 * F)
     Wr = als_ref.fcls_w(X.astype(np.float64), H0.astype(np.float64), 1.0)
-    A, B = Wr.T @ X.astype(np.float64), Wr.T @ Wr
+    A, B = scale * (Wr.T @ X.astype(np.float64)), scale * (Wr.T @ Wr)
     A[1] -= 0.6 * A[1].max()  # force active bounds in the basis rows
     plan = _plan(X, W0, H0, 1.0, lam)
     plan.AB.copy_(torch.from_numpy(np.concatenate([A, B], axis=1).ravel()))

@@ -1,0 +1,14 @@
+#!/bin/bash
+# cfg5 MX (identity-block rotation, LDS exchange of the best mask): parity of variants 7 / 8, A/B
+set -o pipefail
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+D=gpurun_out/${1:-als_mx3}; mkdir -p $D
+T="timeout -k 10 300 python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread"
+CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_diag.so CNMF_ALS_OCC=7 CNMF_ALS_PRIO=2 $T tests/test_gpu_als.py > $D/pytest_als_v7.log 2>&1 || exit 1
+CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_diag.so CNMF_ALS_OCC=8 $T tests/test_gpu_als.py -k persistent > $D/pytest_als_v8.log 2>&1 || exit 1
+B="timeout -k 10 200 python -u bench.py --solver als --steps 200 --warmup 50 --no-cpu"
+for r in 1 2; do
+  CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_diag.so CNMF_ALS_OCC=7 CNMF_ALS_PRIO=2 $B > $D/als_v7p2_r$r.json 2> $D/als_v7p2_r$r.err || exit 1
+  CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_diag.so CNMF_ALS_OCC=8 $B > $D/als_v8_r$r.json 2> $D/als_v8_r$r.err || exit 1
+done
+echo "exit=0"

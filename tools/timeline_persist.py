@@ -161,6 +161,14 @@ def main():
         used = hs[:, :, 1].sum(axis=1) > 0
         summary["hstep_bpp_iters_per_row_last_calls"] = hs[used][-5:, :, 0].tolist()
         summary["hstep_kcycles_per_row_last_calls"] = (hs[used][-5:, :, 1] / 1e3).round(1).tolist()
+        fp = getattr(lib, "cnmf_debug_hstep_phases", None)
+        if fp is not None:  # the wave H-step's phases per row: setup, gather, PCR, check (k cycles)
+            fp.argtypes = [ctypes.c_void_p]
+            fp.restype = ctypes.c_int
+            pb = np.zeros(64 * 4 * 4, dtype=np.uint64)
+            _lib.check(fp(pb.ctypes.data), "hstep phases")
+            ph = pb.reshape(64, 4, 4).astype(np.int64)
+            summary["hstep_phase_kcycles_setup_gather_pcr_check_last_calls"] = (ph[used][-3:] / 1e3).round(2).tolist()
     print(json.dumps(summary), flush=True)
     for r in rows[:5]:
         print(json.dumps({k: round(v, 2) if isinstance(v, float) else v for k, v in r.items()}), flush=True)

@@ -7925,15 +7925,18 @@ struct WaLaunch {
   int64_t G, n_tiles;
   size_t lds;
 };
-// workgroups per CU of the persistent ALS (CNMF_ALS_OCC=1|2, default 2: two waves per SIMD hide the
-// fp64 and LDS latencies of the W-step, at 256 registers per lane and PD = 2; measured on one box,
-// cfg5: 146.6 us per iteration at 1, 123.1 us at 2, profiles/r02/session5/als_iter)
-// (diagnostic build: CNMF_ALS_OCC=1 one workgroup per CU, =3 one per CU with Hᵀ in VGPRs (HREG),
-// =4 two per CU with phase 1 on the matrix cores (MF), =5 one per CU with MF, =6 two per CU with
-// MF and its B operand from LDS (MFL))
+// The persistent ALS kernel: the W-step on the matrix cores (MX), two workgroups per CU (two waves
+// per SIMD hide the MFMA, fp64 and LDS latencies, at 256 registers per lane and PD = 2) and the
+// issue-priority ladder (2 steps per band).  Same-box A/B (profiles/r04/als_mx/): the VALU W-step
+// 122.8 us per iteration, MX 107.7, + the ladder 105, + the Jacobi H-step 101.5, + the identity-block
+// rotations and the LDS exchange of the best mask 97.3.
+// (diagnostic build, CNMF_ALS_OCC: 7 the product; 2 the VALU W-step at two workgroups per CU,
+// 1 one per CU, 3 one per CU with Hᵀ in VGPRs (HREG), 4 two per CU with phase 1 alone on the matrix
+// cores (MF), 5 one per CU with MF, 6 MF with its B operand from LDS (MFL), 8 MX at one per CU;
+// CNMF_ALS_PRIO the ladder's band, 0 = off)
 static int wa_variant() {
-  static const int v = diag_env("CNMF_ALS_OCC") ? atoi(diag_env("CNMF_ALS_OCC")) : 2;
-  return (v >= 1 && v <= 8) ? v : 2;
+  static const int v = diag_env("CNMF_ALS_OCC") ? atoi(diag_env("CNMF_ALS_OCC")) : 7;
+  return (v >= 1 && v <= 8) ? v : 7;
 }
 static int wa_occ() {
   const int v = wa_variant();
@@ -7957,15 +7960,15 @@ static PassFn wa_fn(bool multi = false) {
   if (wa_variant() == 6)
     return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, true, true>)
                  : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, true, true>);
-  if (wa_variant() == 7)
-    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, false, false, true>)
-                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, false, false, true>);
+  if (wa_variant() == 2)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
   if (wa_variant() == 8)
     return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true, false, false, false, true>)
                  : reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, false, false, false, false, true>);
 #endif
-  return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true>)
-               : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2>);
+  return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, false, false, true>)
+               : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, false, false, true>);
 }
 static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false) {
   const int PD = wa_pd();
@@ -8022,7 +8025,7 @@ static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, doubl
   pa.delta2 = sum_to_one * sum_to_one;
   pa.lam = smoothness;
   pa.xctl = xctl;
-  pa.prio = diag_env("CNMF_ALS_PRIO") ? atoi(diag_env("CNMF_ALS_PRIO")) : 0;  // steps per ladder band
+  pa.prio = diag_env("CNMF_ALS_PRIO") ? atoi(diag_env("CNMF_ALS_PRIO")) : 2;  // steps per ladder band
   void* args[] = {&pa};
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn(multi)), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));

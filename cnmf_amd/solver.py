@@ -768,9 +768,10 @@ class ALSPlan(MUPlan):
 
     def describe(self) -> str:
         if self.persistent:
-            return ("als_iter_wt_kernel<PD=2, 2 workgroups per CU>: wave "
-                    "tiles of 16 samples, 4-wave workgroups, in-launch reduction and H-step (one-wave "
-                    "block-cyclic-reduction NNLS solves, every workgroup)")
+            return ("als_iter_wt_kernel<PD=2, 2 workgroups per CU, MX>: wave tiles of 16 samples, "
+                    "the W-step on the matrix cores (c = Hx and the 16 passive sets in fp64 MFMA), "
+                    "in-launch reduction and H-step (one-wave BPP NNLS rows: Jacobi sweeps when "
+                    "10*lambda <= B_jj/20, else block cyclic reduction; every workgroup)")
         return "ALS W-step pass + cnmf_reduce_partials + als_basis_kernel per iteration"
 
     def tune(self, *args, **kwargs) -> dict:

@@ -5079,6 +5079,9 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #else
 #define HS_MARK(p) ((void)0)
 #endif
+      // Jacobi (below) or the block PCR: decided per row from B_jj
+      const double rho = 10.0 * lam / bjj;
+      const bool jac = rho <= 0.05;
       double rb[2], rd[2], re1[2], re2[2], xf[2];
       bool pas[2];
 #pragma unroll
@@ -5095,11 +5098,24 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           re1[c] = le1[c];
           re2[c] = le2[c];
           pas[c] = sH[j * F + f] > 0.0;
-          vb[f] = rb[c];
-          d0[f] = rd[c];
-          e1[f] = re1[c];
-          e2[f] = re2[c];
+          if (!jac) {  // the PCR's gathers read the row from LDS
+            vb[f] = rb[c];
+            d0[f] = rd[c];
+            e1[f] = re1[c];
+            e2[f] = re2[c];
+          }
         }
+      }
+      // neighbour indices clamped into the row (their coefficients are zero there): branch-free
+      // sweeps and checks
+      int fm1[2], fp1[2], fm2[2], fp2[2];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int f = min(lane + 64 * c, F - 1);
+        fm1[c] = max(f - 1, 0);
+        fm2[c] = max(f - 2, 0);
+        fp1[c] = min(f + 1, F - 1);
+        fp2[c] = min(f + 2, F - 1);
       }
       int alpha = 3, beta = F + 1;  // BPP control (wave-uniform)
       // Jacobi: the row's Hessian M = B_jj·I + λ·DᵀD has off-diagonal row sums at most 10λ (the
@@ -5109,8 +5125,6 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // point in a few steps (bound: ρ^nsw <= 2^-55, and a sweep that changes no bit ends early) —
       // the same solve as the block PCR below at a fraction of its per-row cost (two LDS round trips
       // per sweep instead of six shuffle steps of 2x2 blocks and the passive-set compression).
-      const double rho = 10.0 * lam / bjj;
-      const bool jac = rho <= 0.05;
       int nsw = 0;
       for (double r = 1.0; jac && r > 0x1p-55; r *= rho) ++nsw;
       double rinv[2] = {1.0 / rd[0], 1.0 / rd[1]};
@@ -5128,16 +5142,12 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           bool chg = false;
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            const int f = lane + 64 * c;
-            double xn = 0.0;
-            if (f < F && pas[c]) {
-              double r = rb[c];
-              if (f >= 1) r = fma(-lm1[c], vx[f - 1], r);
-              if (f + 1 < F) r = fma(-re1[c], vx[f + 1], r);
-              if (f >= 2) r = fma(-lm2[c], vx[f - 2], r);
-              if (f + 2 < F) r = fma(-re2[c], vx[f + 2], r);
-              xn = r * rinv[c];
-            }
+            double r = rb[c];
+            r = fma(-lm1[c], vx[fm1[c]], r);
+            r = fma(-re1[c], vx[fp1[c]], r);
+            r = fma(-lm2[c], vx[fm2[c]], r);
+            r = fma(-re2[c], vx[fp2[c]], r);
+            const double xn = pas[c] ? r * rinv[c] : 0.0;  // (pas is false past F)
             chg = chg || xn != xf[c];
             xf[c] = xn;
           }
@@ -5248,16 +5258,14 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           bad[c] = false;
           if (f < F) {
             const double x = xf[c];
-            if (pas[c]) {
-              bad[c] = x < 0.0;
-            } else {
-              double y = rd[c] * x - rb[c];
-              if (f + 1 < F) y += re1[c] * vx[f + 1];
-              if (f >= 1) y += e1[f - 1] * vx[f - 1];
-              if (f + 2 < F) y += re2[c] * vx[f + 2];
-              if (f >= 2) y += e2[f - 2] * vx[f - 2];
-              bad[c] = y < 0.0;
-            }
+            // (off P: the dual y = (M x − b)_f, its neighbour terms with the clamped indices
+            // zero-weighted at the row's ends)
+            double y = rd[c] * x - rb[c];
+            y += re1[c] * vx[fp1[c]];
+            y += lm1[c] * vx[fm1[c]];
+            y += re2[c] * vx[fp2[c]];
+            y += lm2[c] * vx[fm2[c]];
+            bad[c] = pas[c] ? x < 0.0 : y < 0.0;
           }
         }
         const uint64_t bb0 = __ballot(bad[0]), bb1 = __ballot(bad[1]);

@@ -76,6 +76,9 @@ _SIGS = {
                                    _i32, _i32, _f64, _f64, _vp, _i32, _vp]),
     "cnmf_als_iterations_multi": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                          _i64, _i32, _i32, _f64, _f64, _vp, _vp, _i32, _vp]),
+    "cnmf_als_persist_workgroups": (_i64, [_i64, _i32, _i32, _i32, _i32]),
+    "cnmf_als_fit_tol": (_i32, [_i32, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                                _i64, _i32, _i32, _f64, _f64, _vp, _vp, _i32, _vp]),
     "cnmf_normalise": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _i32, _vp]),
     "cnmf_mu_shard_step": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _i64, _i32,
                                   _i32, _f64, _f64, _f64, _f64, _i32, _i32, _vp]),

@@ -6686,14 +6686,17 @@ constexpr int L_STG = 0;                                        // [NWV][XSTR]
 constexpr int L_RED = L_STG + wt::NWV * G4::XSTR;               // [NWV][NL][NACC] fp32
 constexpr int L_H = L_RED + wt::NWV * NL * NACC * 4;            // H fp64 [K][F]
 constexpr int L_AB = L_H + K * F * 8;                           // AB fp64 [K][V]
-constexpr int L_HT = L_AB + NOUT * 8;                           // Hᵀ fp64 [NL·NQ][K], rows >= F zero
+constexpr int L_HT = L_AB + (NOUT + 2) * 8;                     // Hᵀ fp64 [NL·NQ][K], rows >= F zero
 constexpr int L_HHT = L_HT + NL * NQ * K * 8;                   // HHᵀ fp64 [K][K]
 // passive-set table, masks at a stride of TSTR doubles (18: the four masks a quad reads with one
 // ds_read_b128 land on disjoint banks; at 16 the masks e and e + 2 shared them), then 16 flags
 constexpr int TSTR = 18;
 constexpr int L_TAB = L_HHT + K * K * 8;
 constexpr int L_FLAG = L_TAB + (16 * TSTR + 16) * 8;            // 4 ints
-constexpr int L_HS = (L_FLAG + 16 + 15) / 16 * 16;              // als_hstep's arrays (als_lds_bytes)
+constexpr int L_LOSS = (L_FLAG + 16 + 15) / 16 * 16;            // TOL: [NWV] wave loss sums, init, prev
+constexpr int L_WSTG = L_LOSS + 8 * 8;                          // TOL: [NWV] the old W tile (256 B)
+constexpr int L_LACC = L_WSTG + wt::NWV * 256;                  // TOL: [NWV][64] the lanes' loss sums
+constexpr int L_HS = L_LACC + wt::NWV * 64 * 8;                 // als_hstep's arrays (als_lds_bytes)
 static_assert(L_RED % 16 == 0 && L_HT % 16 == 0 && L_HS % 16 == 0, "16-byte aligned LDS regions");
 static_assert(NOUT * 8 >= wt::NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
 }  // namespace wa
@@ -6715,7 +6718,8 @@ struct AlsPersistArgs {
   double delta2;     // sum_to_one²
   double lam;        // smoothness
   uint64_t* xctl;    // MULTI: the cross-rank exchange control block (mu_iter_wt_kernel's protocol)
-  int prio;          // diag (CNMF_ALS_PRIO): the issue-priority ladder over an iteration's steps
+  int prio;          // the issue-priority ladder's band (steps; 0 = off)
+  double* tolctl;    // TOL: the tolerance-test control block (cnmf_mu_fit_tol's layout)
 };
 
 // Hᵀ (fp64, the lanes' feature blocks), HHᵀ (fp64; 16 threads per entry, fixed xor tree) and the
@@ -6789,13 +6793,24 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
 //   phase 3  A[g ^ ρ][4ks + g] += x·w[s][g ^ ρ], B[g][g ^ ρ] += w[s][g]·w[s][g ^ ρ] (rotated, fp32 per
 //            lane); the end of the iteration sums the 16 lanes of a row and un-rotates into the
 //            reduction's layout.
-template <int PD, int OCC, bool MULTI = false, bool HREG = false, bool MF = false, bool MFL = false, bool MX = false>
+//
+// TOL (MX only; cnmf_als_fit_tol): the tolerance test of oracle/als_ref.py (SK:872-884's rule) on the
+// device, as mu_iter_wt_kernel's: in iteration g + 1 (g % 10 == 0) every lane also accumulates
+// ‖x − w·H‖² of the state after g iterations — x and H_g are the pass's, W_g is the tile's W read
+// with X (every TOL step prefetches it: the W-step itself never reads W) — carried as one more
+// column of the partial rows; the top combiner applies the test, and on a stop every workgroup leaves
+// with H_g (this iteration's H-step not applied) while the loss iterations' copies of W_g in the
+// snapshot buffer give the host W_g.
+template <int PD, int OCC, bool MULTI = false, bool HREG = false, bool MF = false, bool MFL = false, bool MX = false,
+          bool TOL = false>
 __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) {
   using namespace wt;
   using G4 = Geo<4>;
+  static_assert(!TOL || MX, "the device tolerance test is the MX kernel's");
   constexpr int KK = wa::K, NL = wa::NL, NQ = wa::NQ, V = wa::V, NOUT = wa::NOUT, NACC = wa::NACC;
+  constexpr int NOUTT = NOUT + (TOL ? 1 : 0);  // partial-row width: + the loss of the checked state
   constexpr int XBW = G4::XBW, XSTR = G4::XSTR, PFW = G4::PFW, LASTL = G4::LASTL;
-  constexpr int PFS = PFW;   // loads per prefetch set: the X tile (W is never read)
+  constexpr int PFS = PFW + (TOL ? 1 : 0);  // loads per prefetch set: the X tile (+ TOL: its old W)
   constexpr int KP = KK / 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
@@ -6824,6 +6839,29 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   uint32_t* cnt_top = a.cnt + CNT_TOP;
   uint32_t* flag = a.cnt + CNT_FLAG;
   uint32_t* err = a.cnt + CNT_ERR;
+  // TOL: the launch's first global iteration, the test's error at init and previous error (every
+  // workgroup tracks them itself), the snapshot buffer of W_g, the wave's old-W staging
+  // (uniform values in SGPRs, and each lane's loss sum in LDS: no long-lived VGPR in the streaming
+  // loop, whose spill reloads would wait on — drain — the prefetch)
+  const int it0 = TOL ? __builtin_amdgcn_readfirstlane((int)ld_sc1(a.tolctl + TC_IT0)) : 0;
+  const double tolv = TOL ? ld_sc1(a.tolctl + TC_TOL) : 0.0;
+  double* sLoss = reinterpret_cast<double*>(smem + wa::L_LOSS);
+  double* lacc = reinterpret_cast<double*>(smem + wa::L_LACC) + 64 * w + l;
+  if (TOL) *lacc = 0.0;
+  if (TOL && t == 0) {
+    sLoss[4] = ld_sc1(a.tolctl + TC_INIT);
+    sLoss[5] = ld_sc1(a.tolctl + TC_PREV);
+  }
+  float* wsnap = nullptr;
+  if (TOL) {
+    const long long wp = __double_as_longlong(ld_sc1(a.tolctl + TC_WSNAP));
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)(wp & 0xFFFFFFFFll));
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(wp >> 32));
+    wsnap = reinterpret_cast<float*>(((unsigned long long)hi << 32) | lo);
+  }
+  unsigned char* wstg = smem + wa::L_WSTG + w * 256;
+  unsigned char* Wb = reinterpret_cast<unsigned char*>(a.W);
+  int cur_it = 0;  // the iteration the streaming loop is in
 
   // ---- the basis for the first iteration, Hᵀ / HHᵀ / table, the staging pad
   for (int i = t; i < KK * wa::F; i += NT) sH[i] = a.H64[i];
@@ -6839,19 +6877,15 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   constexpr bool MXR = MX && OCC == 1;
   double hx[MXR ? NQ : 1];
   const double* hxl = reinterpret_cast<const double*>(smem + wa::L_HT) + 4 * gm + (l & 3);  // + 16·ks
-  double tx[MX ? 4 : 1];
-  bool vx[MX ? 4 : 1];
+  // (the FCLS A operands and mask flags are read from the table per tile: long-lived registers here
+  // made the compiler reload spilled values from scratch inside the streaming loop, whose waits
+  // then drain the prefetch)
+  const double* txl = sTab + (l & 3) * wa::TSTR + ((((l & 15) >> 2) ^ (l & 3)) << 2) + gm;  // + 4·TSTR·b'
   auto load_h = [&]() {
     if constexpr (MX) {
       if constexpr (MXR) {
 #pragma unroll
         for (int ks = 0; ks < NQ; ++ks) hx[ks] = hxl[16 * ks];
-      }
-#pragma unroll
-      for (int bp = 0; bp < 4; ++bp) {
-        const int i = l & 15;
-        tx[bp] = sTab[(4 * bp + (i & 3)) * wa::TSTR + (((i >> 2) ^ (i & 3)) << 2) + gm];
-        vx[bp] = sTab[16 * wa::TSTR + 4 * bp + gm] != 0.0;
       }
     }
     if constexpr (HREG) {
@@ -6883,18 +6917,23 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
 #pragma unroll
     for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
     ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
+    if constexpr (TOL) ld16(pf[PFW], l < 16 ? Wb + (size_t)tile * 256 + 16 * l : xs);  // the tile's W
   };
   auto stage = [&](const u32x4 (&pf)[PFS]) {
     const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
     stage_rec<0, PFW - 1>(addr, pf);
     if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
+    if constexpr (TOL)
+      if (l < 16) st16<0>((unsigned)(uintptr_t)(wstg + 16 * l), pf[PFW]);
   };
 
   u32x4 pf[PD][PFS];
   // every body stores its W tile (one store): after each of the first PD sets one dummy store (to this
   // workgroup's partial row, rewritten at the iteration's end) keeps the count of younger operations
-  // at a step's wait exact from the first set on (mu_iter_wt_kernel's streamed-W rule)
-  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUT) + 64 * w + l;
+  // at a step's wait exact from the first set on (mu_iter_wt_kernel's streamed-W rule).  TOL: the W
+  // tile a set loads was stored >= PD steps before (the host keeps nbt >= 2·PD + 1), and the loss
+  // iterations' snapshot stores only add younger operations (the waits get stricter, never short).
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
@@ -6920,10 +6959,16 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   // MX: the identity block — A row i = (g = i % 4, component (i / 4) ^ (i % 4)) of I — turns c[g][s]
   // into the rotated copies c[g ^ ρ][s] in the D registers (exact: one product by 1, three zeros)
   const double tid = ((((l & 15) >> 2) ^ (l & 3)) == gm) ? 1.0 : 0.0;
+  // the wave's exchange scratch (best objective / mask, the new W row): its reduction rows, free
+  // while the tiles stream (the x slot stays intact for phase 3); phase 3's lane roles
+  unsigned char* xscr = reinterpret_cast<unsigned char*>(red + w * NL * NACC);
+  const int s4 = l & 3, g3 = l >> 2;
+  const int f5 = g3 + 80 < wa::F ? g3 + 80 : wa::F - 1;  // the 6th feature (g3 = 0 only; else masked)
+  const float v5 = g3 + 80 < wa::F ? 1.f : 0.f;
   auto wbody_mx = [&](int i) {
     const int64_t tile = gw + (int64_t)NW * i;
-    // phase 1: c[g][s] on lane (s, g); three accumulation chains summed in a fixed order
     const float* xr = reinterpret_cast<const float*>(stg) + sm * wa::F + gm;
+    // phase 1: c[g][s] on lane (s, g); three accumulation chains summed in a fixed order
     float xv[NQ];
 #pragma unroll
     for (int ks = 0; ks < NQ; ++ks) xv[ks] = xr[4 * ks];
@@ -6938,14 +6983,50 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     const double cs = ((m0 + m1) + m2) + a.delta2;  // c[gm][sm] + δ²
     // c rotated: cr[ρ] = c[gm ^ ρ][sm]
     const f64x4 cr = __builtin_amdgcn_mfma_f64_16x16x4f64(tid, cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+    if constexpr (TOL) {
+      if ((it0 + cur_it) % 10 == 0) {
+        // a loss iteration: ‖x − w·H‖² of the state after it0 + cur_it iterations, per sample as
+        // ‖x‖² − 2 w·(Hx) + wᵀ(HHᵀ)w in fp64 (W_g: the tile's W as loaded with X; Hx = c − δ² of
+        // the pass, H_g's Gram in LDS — the terms agree to ~1e-11 of the residual at a 1e-5 fit,
+        // below the test's 1e-4 steps): ‖x‖² over the lane's features, the rest on lane g = 0,
+        // whose rotation is the identity.  W_g's copy goes to the snapshot buffer (a stop here
+        // hands the host W_g).
+        const float4 wo = *reinterpret_cast<const float4*>(wstg + 16 * sm);
+        int so = 4 * sm + gm;  // (opaque: recomputed here, not a loop-invariant 64-bit address)
+        asm volatile("" : "+v"(so));
+        wsnap[(size_t)tile * (16 * KK) + so] = gm == 0 ? wo.x : (gm == 1 ? wo.y : (gm == 2 ? wo.z : wo.w));
+        double xx = 0.0;
+#pragma unroll
+        for (int ks = 0; ks < NQ; ++ks) {
+          const double xd = 4 * ks + gm < wa::F ? (double)xv[ks] : 0.0;
+          xx = fma(xd, xd, xx);
+        }
+        if (gm == 0) {
+          const double* hh = reinterpret_cast<const double*>(smem + wa::L_HHT);
+          const double w4[4] = {(double)wo.x, (double)wo.y, (double)wo.z, (double)wo.w};
+          double cross = 0.0, quad = 0.0;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            cross = fma(w4[q], cr[q] - a.delta2, cross);
+            double hw = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hw = fma(hh[4 * q + r], w4[r], hw);
+            quad = fma(w4[q], hw, quad);
+          }
+          xx = fma(-2.0, cross, xx + quad);
+        }
+        *lacc += xx;
+      }
+    }
     // FCLS: the 16 masks' solutions, lane (s, g) block b' = mask 4b' + g (register ρ = component ρ ^ g);
     // the lane's masks ascend with b', so a strict < keeps the lowest of tied masks
     double bestf = 1.0;
     int bestm = 16;
 #pragma unroll
     for (int bp = 0; bp < 4; ++bp) {
-      const f64x4 v = __builtin_amdgcn_mfma_f64_16x16x4f64(tx[bp], cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
-      const bool feas = vx[bp] & (v[0] >= 0.0) & (v[1] >= 0.0) & (v[2] >= 0.0) & (v[3] >= 0.0);
+      const f64x4 v = __builtin_amdgcn_mfma_f64_16x16x4f64(txl[4 * wa::TSTR * bp], cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+      const bool ok = sTab[16 * wa::TSTR + 4 * bp + gm] != 0.0;
+      const bool feas = ok & (v[0] >= 0.0) & (v[1] >= 0.0) & (v[2] >= 0.0) & (v[3] >= 0.0);
       const double f = -0.5 * fma(cr[3], v[3], fma(cr[2], v[2], fma(cr[1], v[1], cr[0] * v[0])));
       const bool take = feas & (f < bestf);
       bestf = take ? f : bestf;
@@ -6953,9 +7034,9 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
     // the sample's four lanes exchange their best through the wave's staging slot (its x is in
     // registers; in-order LDS inside the wave) and each takes the least (objective, mask)
-    double* xf_ = reinterpret_cast<double*>(stg);
-    int* xm_ = reinterpret_cast<int*>(stg + 512);
-    float* xw_ = reinterpret_cast<float*>(stg + 768);
+    double* xf_ = reinterpret_cast<double*>(xscr);
+    int* xm_ = reinterpret_cast<int*>(xscr + 512);
+    float* xw_ = reinterpret_cast<float*>(xscr + 768);
     xf_[4 * sm + gm] = bestf;
     xm_[4 * sm + gm] = bestm;
     {
@@ -6979,18 +7060,30 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
     const float wn = (float)fmax(wn64, 0.0);
     a.W[(size_t)tile * (16 * KK) + 4 * sm + gm] = wn;  // the tile's 256 contiguous bytes
-    // phase 3 with the sample's new row (through the slot)
+    // phase 3, regrouped: lane (s4 = l % 4, g3 = l / 4) takes the tile's samples 4j + s4 (j < 4) and
+    // the features g3 + 16k (k < 6; k = 5 only for g3 = 0), x read again from the slot: 24 + 4 fp32
+    // accumulators per lane instead of the (s, g) layout's 88 and no x registers across the FCLS —
+    // the streaming loop then keeps every value in registers (a spill reload there waits on, and
+    // drains, the prefetch)
     xw_[4 * sm + gm] = wn;
-    const float4 w4 = *reinterpret_cast<const float4*>(xw_ + 4 * sm);
-    const f2 wp0 = f2{w4.x, w4.y}, wp1 = f2{w4.z, w4.w};
 #pragma unroll
-    for (int ks = 0; ks < NQ; ++ks) {
-      const f2 xx = f2{xv[ks], xv[ks]};
-      acc[ks][0] = __builtin_elementwise_fma(xx, wp0, acc[ks][0]);
-      acc[ks][1] = __builtin_elementwise_fma(xx, wp1, acc[ks][1]);
+    for (int j4 = 0; j4 < 4; ++j4) {
+      const int s3 = 4 * j4 + s4;
+      const float4 w4 = *reinterpret_cast<const float4*>(xw_ + 4 * s3);
+      const float wr = xw_[4 * s3 + (g3 & 3)];
+      const f2 wp0 = f2{w4.x, w4.y}, wp1 = f2{w4.z, w4.w};
+      const float* xs3 = reinterpret_cast<const float*>(stg) + wa::F * s3;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        float xx1 = xs3[k < 5 ? g3 + 16 * k : f5];
+        if (k == 5) xx1 *= v5;
+        const f2 xx = f2{xx1, xx1};
+        acc[k][0] = __builtin_elementwise_fma(xx, wp0, acc[k][0]);
+        acc[k][1] = __builtin_elementwise_fma(xx, wp1, acc[k][1]);
+      }
+      accB[0] = __builtin_elementwise_fma(f2{wr, wr}, wp0, accB[0]);
+      accB[1] = __builtin_elementwise_fma(f2{wr, wr}, wp1, accB[1]);
     }
-    accB[0] = __builtin_elementwise_fma(f2{wn, wn}, wp0, accB[0]);
-    accB[1] = __builtin_elementwise_fma(f2{wn, wn}, wp1, accB[1]);
   };
   auto wbody = [&](int i) {
     if constexpr (MX) {
@@ -7104,21 +7197,24 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     const bool last_it = it + 1 == a.n_iter;
     // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
     if constexpr (MX) {
-      // the 16 sample lanes of row g summed; the row's first lane writes features 4ks + g
-      const bool wr = sm == 0;
+      // the quad's four sample groups summed (lanes 4·g3 .. 4·g3 + 3); its first lane writes the
+      // features g3 + 16k and, g3 < 4, the WᵀW row g3
+      auto qsum = [&](float v) {
+        v += dppf<0xB1>(v);         // quad_perm [1,0,3,2]
+        return v + dppf<0x4E>(v);   // quad_perm [2,3,0,1]
+      };
+      const bool wr = s4 == 0;
 #pragma unroll
-      for (int ks = 0; ks < NQ; ++ks) {
-        const float4 v = make_float4(sum_over_row16(acc[ks][0].x), sum_over_row16(acc[ks][0].y),
-                                     sum_over_row16(acc[ks][1].x), sum_over_row16(acc[ks][1].y));
-        const int f = 4 * ks + gm;
+      for (int k = 0; k < 6; ++k) {
+        const float4 v = make_float4(qsum(acc[k][0].x), qsum(acc[k][0].y), qsum(acc[k][1].x), qsum(acc[k][1].y));
+        const int f = g3 + 16 * k;
         if (wr && f < wa::F) {
           const int ee = f / NQ;
           *reinterpret_cast<float4*>(red + (w * NL + ee) * NACC + (f - NQ * ee) * KK) = v;
         }
       }
-      const float4 v = make_float4(sum_over_row16(accB[0].x), sum_over_row16(accB[0].y),
-                                   sum_over_row16(accB[1].x), sum_over_row16(accB[1].y));
-      if (wr) *reinterpret_cast<float4*>(red + (w * NL + gm) * NACC + NQ * KK) = v;
+      const float4 v = make_float4(qsum(accB[0].x), qsum(accB[0].y), qsum(accB[1].x), qsum(accB[1].y));
+      if (wr && g3 < 4) *reinterpret_cast<float4*>(red + (w * NL + g3) * NACC + NQ * KK) = v;
     } else {
       // the sums over the lanes of one feature group: lanes ≡ e (mod 4), or (MF) the 16 lanes of a row
       auto ssum = [&](float v) { return MF ? sum_over_row16(v) : sum_over_samples<NL>(v); };
@@ -7133,9 +7229,18 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       if (wr) *reinterpret_cast<float4*>(rw + NQ * KK) = v;
     }
     zero_acc();
+    const bool loss_it = TOL && ((it0 + it) % 10 == 0);  // this iteration checked the state after it0 + it
+    if constexpr (TOL) {  // the wave's loss sum (zero outside loss iterations), fixed xor tree
+      const double v = wave_sum(*lacc);
+      if (l == 0) sLoss[w] = v;
+      *lacc = 0.0;
+    }
     __syncthreads();
     {
-      double* prow = a.partials + (size_t)b * NOUT;
+      double* prow = a.partials + (size_t)b * NOUTT;
+      if (TOL && t == 0)
+        __hip_atomic_store(prow + NOUT, (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
       for (int o = t; o < NOUT; o += NT) {
         const int j = o / V;
         const int v = o - j * V;
@@ -7155,10 +7260,14 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       sFlag[0] = old == (uint32_t)((it + 1) * gs - 1);
       sFlag[1] = 0;
       sFlag[2] = 1;
+      sFlag[3] = 0;
     }
     __syncthreads();
+    // TOL: the last iteration of the launch waits for the flag too when it checks the tolerance (a
+    // stop there must reach every workgroup before the top applies the last H-step)
+    const bool must_wait = !last_it || loss_it;
     if (sFlag[0]) {  // group combiner
-      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -7167,42 +7276,44 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
-        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAB, a.AB, t);
-        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AB, sAB, err, it, t);  // + the other ranks' AB
+        sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);  // + the other ranks' AB
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t == 0 && !last_it)
-          __hip_atomic_store(flag, (uint32_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (TOL && loss_it && t == 0) {  // the relative-decrease test on the state after it0 + it
+          const int gi = it0 + it;
+          const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+          const int slot = gi / 10;
+          if (slot < (int)ld_sc1(a.tolctl + TC_CAP)) st_sc1(a.tolctl + TC_ERRS + slot, errv);
+          st_sc1(a.tolctl + TC_NERR, (double)(slot + 1));
+          if (gi == 0) {
+            sLoss[4] = sLoss[5] = errv;
+            st_sc1(a.tolctl + TC_INIT, errv);
+            st_sc1(a.tolctl + TC_PREV, errv);
+          } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
+            sFlag[3] = 1;
+          } else {
+            sLoss[5] = errv;
+            st_sc1(a.tolctl + TC_PREV, errv);
+          }
+        }
+        if (TOL && loss_it) __syncthreads();  // sFlag[3] (the decision) for the whole workgroup
+        if (t == 0 && must_wait)
+          __hip_atomic_store(flag, (uint32_t)(it + 1) | (sFlag[3] ? FLAG_STOP : 0u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         TL_PUB(it);
       }
     }
     const bool top = sFlag[1] != 0;
-    if (last_it) {
-      alive = false;
-      if (!top) return;
-      // the last combiner of the launch: the last H-step, then the basis state for the host
-      wa_update_basis(t, a.lam, a.delta2);
-      for (int o = t; o < KK * wa::F; o += NT) a.H64[o] = sH[o];
-      for (int o = t; o < wa::F * KK; o += NT) a.Ht[o] = reinterpret_cast<const double*>(smem + wa::L_HT)[o];
-      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + wa::L_HHT)[t];
-      for (int o = t; o < ALS_TAB; o += NT)  // the global table keeps the stride of 16
-        a.table[o] = o < 256 ? sTab[(o >> 4) * wa::TSTR + (o & 15)] : sTab[16 * wa::TSTR + (o - 256)];
-      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (t == 0) {
-        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (MULTI)  // the next launch's generations follow this one's
-          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    if (!top) {
+    if (!top && must_wait) {
       if (t == 0) {
         const uint32_t want = (uint32_t)(it + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t f;
         while (true) {  // the flag and the error word in one batch: one round trip per round
           const uint32_t ev = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+          f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((f & ~FLAG_STOP) >= want) break;
           if (ev != 0u) {
             sFlag[2] = 0;
             break;
@@ -7214,14 +7325,66 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
           }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (TOL && (f & FLAG_STOP)) sFlag[3] = 1;
       }
       __syncthreads();
       if (!sFlag[2]) {
         alive = false;
         return;
       }
-      for (int o = t; o < NOUT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+    }
+    // the basis state for the host (the last combiner of the launch, or the top of a stop)
+    auto write_state = [&]() {
+      for (int o = t; o < KK * wa::F; o += NT) a.H64[o] = sH[o];
+      for (int o = t; o < wa::F * KK; o += NT) a.Ht[o] = reinterpret_cast<const double*>(smem + wa::L_HT)[o];
+      if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + wa::L_HHT)[t];
+      for (int o = t; o < ALS_TAB; o += NT)  // the global table keeps the stride of 16
+        a.table[o] = o < 256 ? sTab[(o >> 4) * wa::TSTR + (o & 15)] : sTab[16 * wa::TSTR + (o - 256)];
+      if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (TOL && sFlag[3]) {
+      // stopped by the tolerance test: the state after it0 + it iterations — H_g (this iteration's
+      // H-step not applied), W_g in the snapshot buffer; the host clears the flag word
+      alive = false;
+      if (!top) return;
+      write_state();
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
+        st_sc1(a.tolctl + TC_STOPPED, 1.0);
+        st_sc1(a.tolctl + TC_IN_SNAP, 1.0);
+        if (MULTI)
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)(it + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (last_it) {
+      alive = false;
+      if (!top) return;
+      // the last combiner of the launch: the last H-step, then the basis state for the host
+      wa_update_basis(t, a.lam, a.delta2);
+      write_state();
+      if (t == 0) {
+        __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!must_wait)  // (else workgroups may still poll it: the host clears it after the launch)
+          __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (TOL) {
+          st_sc1(a.tolctl + TC_DONE, (double)(it0 + a.n_iter));
+          st_sc1(a.tolctl + TC_STOPPED, 0.0);
+        }
+        if (MULTI)  // the next launch's generations follow this one's
+          __hip_atomic_fetch_add(a.xctl + XC_GEN, (uint64_t)a.n_iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (!top) {
+      for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
       __syncthreads();
+      if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
+        const double errv = sqrt(fmax(sAB[NOUT], 0.0));
+        if (it0 + it == 0) sLoss[4] = errv;
+        sLoss[5] = errv;
+      }
     }
     wa_update_basis(t, a.lam, a.delta2);
     load_h();
@@ -7229,6 +7392,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   };
 
   for (int it = 0; it < a.n_iter && alive; ++it) {
+    cur_it = it;
     for (int i0 = 0; i0 < nbp; i0 += PD) {
       if (a.prio) {
         // the ladder: a wave with more steps left issues first, so the two workgroups sharing a CU
@@ -7951,7 +8115,10 @@ static int wa_occ() {
   return (v == 2 || v == 4 || v == 6 || v == 7) ? 2 : 1;
 }
 static int wa_pd() { return wa_occ() == 1 ? 3 : 2; }  // X tiles in flight per wave
-static PassFn wa_fn(bool multi = false) {
+static PassFn wa_fn(bool multi = false, bool tol = false) {
+  if (tol)  // the device tolerance test: the product kernel's TOL form (two workgroups per CU, PD = 2)
+    return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, false, false, true, true>)
+                 : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, false, false, true, true>);
 #ifdef CNMF_DIAG
   if (wa_variant() == 1)
     return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<3, 1, true>)
@@ -7978,17 +8145,23 @@ static PassFn wa_fn(bool multi = false) {
   return multi ? reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, true, false, false, false, true>)
                : reinterpret_cast<PassFn>(&als_iter_wt_kernel<2, 2, false, false, false, false, true>);
 }
-static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false) {
-  const int PD = wa_pd();
+static bool wa_plan(int64_t n_rows, int x_dtype, int F, int k, WaLaunch* out, bool multi = false,
+                    bool tol = false) {
+  const int PD = tol ? 2 : wa_pd();
+  const int occ = tol ? 2 : wa_occ();
   if (x_dtype != CNMF_F32 || F != wt::F || k != wa::K || n_rows <= 0 || n_rows % wa::TSW != 0) return false;
   if (diag_env("CNMF_ALS_PERSIST") && atoi(diag_env("CNMF_ALS_PERSIST")) == 0) return false;
   const int64_t n_tiles = n_rows / wa::TSW;
-  const int64_t G = std::min<int64_t>({(int64_t)device_cus() * wa_occ(), n_tiles / (wt::NWV * (PD + 1)),
+  // tiles per wave: >= 2·PD + 1 — the TOL form re-loads W tiles (a tile's store retires before the
+  // set that re-loads it is waited for, mu_iter_wt_kernel's streamed-W rule), and the plain form
+  // takes the same grid so that a fit whose test never stops is bit-identical to it
+  const int min_nbt = 2 * PD + 1;
+  const int64_t G = std::min<int64_t>({(int64_t)device_cus() * occ, n_tiles / (wt::NWV * min_nbt),
                                        (int64_t)sl::GROUP * sl::MAX_GROUPS});
   if (G < 1) return false;
   const size_t lds = (size_t)wa::L_HS + als_lds_bytes(F, k);
   if (lds > kMaxLds) return false;
-  if (max_resident(wa_fn(multi), lds) < G) return false;
+  if (max_resident(wa_fn(multi, tol), lds) < G) return false;
   *out = WaLaunch{G, n_tiles, lds};
   return true;
 }
@@ -7998,16 +8171,23 @@ int cnmf_als_persistent(int64_t n_rows, int n_features, int k, int x_dtype) {
   return wa_plan(n_rows, x_dtype, n_features, k, &L) ? 1 : 0;
 }
 
+int64_t cnmf_als_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int flags) {
+  WaLaunch L;
+  return wa_plan(n_rows, x_dtype, n_features, k, &L, (flags & 1) != 0, (flags & 2) != 0) ? L.G : 0;
+}
+
 static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
                           double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
                           double* AB, int64_t n_rows, int n_features, int k, double sum_to_one, double smoothness,
-                          uint64_t* xctl, void* const* events, int n_events, void* stream) {
+                          uint64_t* xctl, void* const* events, int n_events, void* stream,
+                          double* tolctl = nullptr) {
   if (n_iter <= 0) return CNMF_OK;
   WaLaunch L;
-  const bool multi = xctl != nullptr;
-  if (!wa_plan(n_rows, x_dtype, n_features, k, &L, multi))
+  const bool multi = xctl != nullptr, tol = tolctl != nullptr;
+  if (!wa_plan(n_rows, x_dtype, n_features, k, &L, multi, tol))
     return set_err(CNMF_ERR_UNSUPPORTED, "the persistent constrained ALS serves fp32 F=81 k=4 with rows a multiple "
-                   "of 16 (n_rows=%lld F=%d k=%d)", (long long)n_rows, n_features, k);
+                   "of 16 and >= %d tiles of 16 rows (n_rows=%lld F=%d k=%d)", wt::NWV * (2 * (tol ? 2 : wa_pd()) + 1),
+                   (long long)n_rows, n_features, k);
   if (!X || !W || !H64 || !Ht || !HHt || !table || !partials || !stage || !counter || !AB)
     return set_err(CNMF_ERR_ARG, "null pointer argument");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
@@ -8034,11 +8214,25 @@ static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, doubl
   pa.lam = smoothness;
   pa.xctl = xctl;
   pa.prio = diag_env("CNMF_ALS_PRIO") ? atoi(diag_env("CNMF_ALS_PRIO")) : 2;  // steps per ladder band
+  pa.tolctl = tolctl;
   void* args[] = {&pa};
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
-  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn(multi)), dim3((unsigned)L.G), dim3(NT), args, L.lds, hs));
+  HIP_CHECK(hipLaunchKernel(reinterpret_cast<const void*>(wa_fn(multi, tol)), dim3((unsigned)L.G), dim3(NT), args,
+                            L.lds, hs));
   if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
+  // TOL: the iteration flag may still hold the last (or the stopping) iteration: cleared in stream order
+  if (tol) HIP_CHECK(hipMemsetAsync(counter + CNT_FLAG, 0, sizeof(uint32_t), hs));
   return CNMF_OK;
+}
+
+int cnmf_als_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                     double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                     double* AB, double* tolctl, int64_t n_rows, int n_features, int k, double sum_to_one,
+                     double smoothness, uint64_t* xctl, void* const* events, int n_events, void* stream) {
+  if (max_iter <= 0) return set_err(CNMF_ERR_ARG, "max_iter must be >= 1");
+  if (!tolctl) return set_err(CNMF_ERR_ARG, "null pointer argument");
+  return als_iterations(max_iter, X, x_dtype, W, H64, Ht, HHt, table, partials, n_parts, stage, counter, AB, n_rows,
+                        n_features, k, sum_to_one, smoothness, xctl, events, n_events, stream, tolctl);
 }
 
 int cnmf_als_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,

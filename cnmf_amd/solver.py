@@ -517,10 +517,7 @@ class MUPlan:
         # this shard's eligibility, asked of the TOL kernel's own plan (bit 1), then agreed over the
         # plan's group: ranks that launched the exchange-plus-tol kernel would wait in
         # the exchange for a rank that took the host loop
-        with torch.cuda.device(self.device):
-            probe = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, self.layout,
-                                                     (1 if xctl is not None else 0) | 2)
-        ok = self.n_rows > 0 and probe > 0 and "wave tiles" in self.describe()
+        ok = self.n_rows > 0 and self._tol_served(xctl is not None)
         if self.world > 1 and agree_max([0.0 if ok else 1.0], self.group, self.device)[0] != 0.0:
             return None
         if not ok:
@@ -533,11 +530,7 @@ class MUPlan:
         host[self._TC["cap"]] = n_tc - self._TC["errs"]
         host[self._TC["wsnap"]] = np.array([self._wsnap.data_ptr()], dtype=np.uint64).view(np.float64)[0]
         tolctl = torch.from_numpy(host).to(self.device)
-        args = (max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
-                _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self._AB),
-                _ptr(tolctl), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H,
-                self.layout, xctl, *_event_array(pass_events), self._stream())
-        fn = self.lib.cnmf_mu_fit_tol
+        fn, args = self._tol_call(max_iter, tolctl, xctl, pass_events)
         cargs = tuple(None if a is None else t(a) if not isinstance(a, ctypes.Array) else a
                       for a, t in zip(args, fn.argtypes))
         state = {}
@@ -554,15 +547,29 @@ class MUPlan:
             agrees the fallback with its peers, as after a failed launch)."""
             if not raise_on_error and state.get("st", -1) < 0:
                 import warnings
-                warnings.warn(f"cnmf_mu_fit_tol: {self.lib.cnmf_last_error().decode()}", RuntimeWarning)
+                warnings.warn(f"{fn.__name__}: {self.lib.cnmf_last_error().decode()}", RuntimeWarning)
                 return None
-            check(state.get("st", -1), "cnmf_mu_fit_tol")
+            check(state.get("st", -1), fn.__name__)
             out = tolctl.cpu().numpy()
             if out[self._TC["stopped"]] != 0 and out[self._TC["in_snap"]] != 0:
                 self.W.copy_(self._wsnap)
             nerr = min(int(out[self._TC["nerr"]]), n_tc - self._TC["errs"])
             return int(out[self._TC["done"]]), [(10 * i, float(out[self._TC["errs"] + i])) for i in range(nerr)]
         return run, finish
+
+    def _tol_served(self, multi: bool) -> bool:
+        """The TOL launch's own plan serves this shape (and layout, and the exchange when multi)."""
+        with torch.cuda.device(self.device):
+            probe = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, self.layout,
+                                                     (1 if multi else 0) | 2)
+        return probe > 0 and "wave tiles" in self.describe()
+
+    def _tol_call(self, max_iter, tolctl, xctl, pass_events):
+        args = (max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter), _ptr(self._AB),
+                _ptr(tolctl), self.n_rows, self.F, self.k, self.l1_W, self.l2_W, self.l1_H, self.l2_H,
+                self.layout, xctl, *_event_array(pass_events), self._stream())
+        return self.lib.cnmf_mu_fit_tol, args
 
     def fit_device_tol(self, max_iter: int, tol: float, pass_events=None):
         """max_iter MU iterations with sklearn's tolerance test (SK:872-884) evaluated on the device:
@@ -777,11 +784,20 @@ class ALSPlan(MUPlan):
     def tune(self, *args, **kwargs) -> dict:
         return {}  # one layout
 
-    def prepare_device_tol(self, *args, **kwargs):
-        return None  # the tolerance test of the ALS runs on the host (its loss is not the MU pass's)
+    def _tol_served(self, multi: bool) -> bool:
+        """cnmf_als_fit_tol's plan serves this shard (the persistent shape with >= 5 tiles per wave)."""
+        with torch.cuda.device(self.device):
+            probe = self.lib.cnmf_als_persist_workgroups(self.n_rows, self.F, self.k, self.xdt,
+                                                         (1 if multi else 0) | 2)
+        return probe > 0
 
-    def fit_device_tol(self, *args, **kwargs):
-        return None
+    def _tol_call(self, max_iter, tolctl, xctl, pass_events):
+        # the TOL launch writes the loss column: rows of n_out + 1 in the same memory
+        args = (max_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht), _ptr(self.HHt),
+                _ptr(self.table), _ptr(self._partials), self.n_parts, _ptr(self.stage), _ptr(self.counter),
+                _ptr(self._AB), _ptr(tolctl), self.n_rows, self.F, self.k, self.delta, self.lam, xctl,
+                *_event_array(pass_events), self._stream())
+        return self.lib.cnmf_als_fit_tol, args
 
     def prepare(self, n_iter: int, pass_events=None):
         """As MUPlan.prepare, for the persistent ALS launch."""

@@ -274,6 +274,23 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
                               uint32_t* counter, double* AB, int64_t n_rows, int n_features, int k,
                               double sum_to_one, double smoothness, uint64_t* xctl, void* const* events,
                               int n_events, void* stream);
+/* Workgroups of the persistent ALS launch for this shape (0: not served).  flags bit 0: the
+ * exchange form (cnmf_als_iterations_multi); bit 1: the tolerance-test form (cnmf_als_fit_tol, which
+ * needs >= 5 tiles of 16 rows per wave). */
+int64_t cnmf_als_persist_workgroups(int64_t n_rows, int n_features, int k, int x_dtype, int flags);
+/* A max_iter constrained-ALS fit with the tolerance test of oracle/als_ref.py (SK:872-884's rule:
+ * ‖X − WH‖ every 10 iterations, stop when (previous − error) / error_at_init < tol) evaluated on the
+ * device: ONE launch of the persistent kernel (replaces the host loop of `run_mu` over
+ * cnmf_als_iterations + a loss pass per 10 iterations).  tolctl: cnmf_tolctl_doubles(max_iter)
+ * doubles laid out as for cnmf_mu_fit_tol (CNMF_TC_*; TC_WSNAP = the address of an N x k fp32
+ * snapshot buffer as a double's bits).  On a stop at g iterations: H64 / Ht / HHt / table hold the
+ * basis after g iterations, the snapshot buffer holds W after g iterations (TC_IN_SNAP = 1: the
+ * caller copies it to W), TC_DONE = g.  xctl: null, or the exchange block (several GPUs, every
+ * rank the same max_iter and tol).  partials / stage / AB: rows of k(F + k) + 1 doubles. */
+int cnmf_als_fit_tol(int max_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht, double* HHt,
+                     double* table, double* partials, int64_t n_parts, double* stage, uint32_t* counter,
+                     double* AB, double* tolctl, int64_t n_rows, int n_features, int k, double sum_to_one,
+                     double smoothness, uint64_t* xctl, void* const* events, int n_events, void* stream);
 
 
 /* ---- weighted / masked MU (oracle/wmu_ref.py).  Per-element weights

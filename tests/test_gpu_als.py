@@ -292,3 +292,51 @@ def test_persistent_als_two_ranks_one_gpu_exchange():
     Wr, Hr, _ = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
                                 max_iter=20, tol=0.0, sum_to_one=1.0, smoothness=0.5)
     assert rel_fro(W, Wr) <= 1e-5 and rel_fro(out[0][1], Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(out[0][1], Hr))
+
+
+# ---- the tolerance test on the device (cnmf_als_fit_tol; VERDICT r3 "missing" #5)
+
+def _host_loop(plan):
+    plan.prepare_device_tol = lambda *a, **k: None  # run_mu's host loop: stretches of 10 + a loss pass
+    return plan
+
+
+def test_persistent_als_device_tol_matches_host_loop_and_oracle():
+    """ONE launch with the test on the device: n_iter, the checked errors, W and H against the host
+    loop (the same iterations: W / H bit-identical, errors to their residuals' precision) and
+    against the oracle's n_iter and factors."""
+    from cnmf_amd.solver import run_mu
+    X, W0, H0 = _mixtures(40000, 81, 4, seed=7)
+    plan = _plan(X, W0, H0, 1.0, 0.5)
+    assert plan.persistent and plan._tol_served(False)
+    n, errs = run_mu(plan, max_iter=300, tol=1e-4, return_errors=True)
+    assert plan.counters_at_rest()
+    host = _host_loop(_plan(X, W0, H0, 1.0, 0.5))
+    n2, errs2 = run_mu(host, max_iter=300, tol=1e-4, return_errors=True)
+    print(f"device tol: n_iter {n} (host {n2}), errors {errs[:3]} .. {errs[-1]}")
+    assert n == n2 and n < 300, (n, n2)
+    assert [g for g, _ in errs] == [g for g, _ in errs2]
+    # (the host's loss pass forms fp32 residuals, the launch fp64 ones: ~3e-8 apart)
+    np.testing.assert_allclose([e for _, e in errs], [e for _, e in errs2], rtol=1e-6)
+    assert np.array_equal(plan.W.cpu().numpy(), host.W.cpu().numpy())
+    assert np.array_equal(plan.H64.cpu().numpy(), host.H64.cpu().numpy())
+    Wr, Hr, nr = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                 max_iter=300, tol=1e-4, sum_to_one=1.0, smoothness=0.5, w_step="enumerate")
+    assert n == nr, (n, nr)
+    W, H = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(H, Hr))
+
+
+def test_persistent_als_device_tol_without_a_stop_is_bit_identical():
+    """A fit whose test never stops runs the same arithmetic as the plain launch (the loss column
+    only adds to the reduction), and the basis state it leaves (Hᵀ, HHᵀ, the table) is the plain one's."""
+    from cnmf_amd.solver import run_mu
+    X, W0, H0 = _mixtures(40000, 81, 4, seed=8)
+    a, b = _plan(X, W0, H0, 1.0, 0.5), _plan(X, W0, H0, 1.0, 0.5)
+    n, errs = run_mu(a, max_iter=30, tol=1e-300, return_errors=True)
+    b.iterate(30)
+    b.check_sync_error()
+    assert n == 30 and [g for g, _ in errs] == [0, 10, 20, 30]
+    for u, v in ((a.W, b.W), (a.H64, b.H64), (a.Ht, b.Ht), (a.HHt, b.HHt), (a.table, b.table)):
+        assert np.array_equal(u.cpu().numpy(), v.cpu().numpy())
+    assert a.counters_at_rest()

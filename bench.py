@@ -457,7 +457,11 @@ def main():
 
     def timed():
         persistent = plan.persistent and (world == 1 or plan.exchange)
-        events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if persistent else 2 * K)]
+        # two events around the whole timed stretch for the single-GPU MU launches too (cfg4's pass +
+        # reduction + update per iteration): an event record between every iteration's launches
+        # stretched cfg4's timed iterations by ~14 us over tune()'s (profiles/r04/e/)
+        whole = persistent or (world == 1 and type(plan).__name__ == "MUPlan" and not plan.shard_steps)
+        events = [torch.cuda.Event(enable_timing=True) for _ in range(2 if whole else 2 * K)]
         stream = torch.cuda.current_stream(dev)
         for e in events:  # creates the HIP events (outside the timed region)
             e.record(stream)
@@ -487,9 +491,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        return persistent, events, elapsed
+        return persistent, events, elapsed, whole
 
-    persistent, events, elapsed = timed()
+    persistent, events, elapsed, whole = timed()
     if getattr(plan, "exchange", False):  # a failed exchange launch: every rank re-times on RCCL
         fail = False
         try:
@@ -504,11 +508,14 @@ def main():
             plan.set_H(H0d)
             plan.iterate(args.warmup)
             torch.cuda.synchronize()
-            persistent, events, elapsed = timed()
+            persistent, events, elapsed, whole = timed()
     plan.check_sync_error()
     if persistent:  # ONE launch ran all K iterations (pass + in-launch reduction + basis update)
         launches = 1
         avg_launch_s = events[0].elapsed_time(events[1]) / 1e3
+    elif whole:  # K iterations of launches between two events: the average iteration
+        launches = K
+        avg_launch_s = events[0].elapsed_time(events[1]) / 1e3 / K
     else:
         launches = K
         avg_launch_s = float(np.mean([events[2 * i].elapsed_time(events[2 * i + 1])

@@ -8660,7 +8660,11 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
     if (events && n_events >= 2) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
     return CNMF_OK;
   }
+  // events: 2·n_iter around each iteration (pass + reduction + update), or (n_events == 2) around the
+  // whole n iterations — no event record between the launches of a timed stretch
   const bool ev = events && n_events >= 2 * n_iter;
+  const bool ev_all = events && !ev && n_events == 2;
+  if (ev_all) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[0]), hs));
   for (int it = 0; it < n_iter; ++it) {  // events around the whole iteration (pass + reduction + update)
     if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it]), hs));
     int st = cnmf_mu_sample_pass(X, x_dtype, W, Ht, HHt, partials, n_rows, n_features, k, l1_W,
@@ -8671,6 +8675,7 @@ int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* 
     if (st) return st;
     if (ev) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[2 * it + 1]), hs));
   }
+  if (ev_all) HIP_CHECK(hipEventRecord(reinterpret_cast<hipEvent_t>(events[1]), hs));
   return CNMF_OK;
 }
 

@@ -127,7 +127,8 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  * events (may be NULL), caller-created hipEvent_t recorded on `stream` for live kernel timing:
  *   persistent: events[0] / events[1] before / after the launch (n_events >= 2);
  *   otherwise : events[2i] / events[2i+1] around iteration i: its pass, reduction and basis
- *               update (n_events >= 2*n_iter).
+ *               update (n_events >= 2*n_iter), or, n_events == 2, events[0] / events[1] around
+ *               all n_iter iterations (no event record between the launches).
  * Persistent shapes: fp32 F = 81, k = 4 / 8 (mu_iter_wt_kernel), and with layout 6 bf16
  * F = 289..320, k = 16, n_rows a multiple of 64 (mu_iter_bfw_kernel, cfg4). */
 int cnmf_mu_iterations(int n_iter, const void* X, int x_dtype, void* W, double* H64, double* Ht,

@@ -6877,15 +6877,20 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   constexpr bool MXR = MX && OCC == 1;
   double hx[MXR ? NQ : 1];
   const double* hxl = reinterpret_cast<const double*>(smem + wa::L_HT) + 4 * gm + (l & 3);  // + 16·ks
-  // (the FCLS A operands and mask flags are read from the table per tile: long-lived registers here
-  // made the compiler reload spilled values from scratch inside the streaming loop, whose waits
-  // then drain the prefetch)
-  const double* txl = sTab + (l & 3) * wa::TSTR + ((((l & 15) >> 2) ^ (l & 3)) << 2) + gm;  // + 4·TSTR·b'
+  // the FCLS A operands (table rows) and the validity of the lane's four masks, per iteration
+  double tx[MX ? 4 : 1];
+  bool vx[MX ? 4 : 1];
   auto load_h = [&]() {
     if constexpr (MX) {
       if constexpr (MXR) {
 #pragma unroll
         for (int ks = 0; ks < NQ; ++ks) hx[ks] = hxl[16 * ks];
+      }
+#pragma unroll
+      for (int bp = 0; bp < 4; ++bp) {
+        const int i = l & 15;
+        tx[bp] = sTab[(4 * bp + (i & 3)) * wa::TSTR + (((i >> 2) ^ (i & 3)) << 2) + gm];
+        vx[bp] = sTab[16 * wa::TSTR + 4 * bp + gm] != 0.0;
       }
     }
     if constexpr (HREG) {
@@ -7024,9 +7029,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     int bestm = 16;
 #pragma unroll
     for (int bp = 0; bp < 4; ++bp) {
-      const f64x4 v = __builtin_amdgcn_mfma_f64_16x16x4f64(txl[4 * wa::TSTR * bp], cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
-      const bool ok = sTab[16 * wa::TSTR + 4 * bp + gm] != 0.0;
-      const bool feas = ok & (v[0] >= 0.0) & (v[1] >= 0.0) & (v[2] >= 0.0) & (v[3] >= 0.0);
+      const f64x4 v = __builtin_amdgcn_mfma_f64_16x16x4f64(tx[bp], cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+      const bool feas = vx[bp] & (v[0] >= 0.0) & (v[1] >= 0.0) & (v[2] >= 0.0) & (v[3] >= 0.0);
       const double f = -0.5 * fma(cr[3], v[3], fma(cr[2], v[2], fma(cr[1], v[1], cr[0] * v[0])));
       const bool take = feas & (f < bestf);
       bestf = take ? f : bestf;

@@ -785,11 +785,8 @@ class ALSPlan(MUPlan):
         return {}  # one layout
 
     def _tol_served(self, multi: bool) -> bool:
-        """cnmf_als_fit_tol's plan serves this shard (the persistent shape with >= 5 tiles per wave).
-        Single GPU only for now: the exchange-plus-tolerance form of the ALS launch has no GPU test
-        yet (ADVICE r3's rule), so sharded fits keep run_mu's host loop."""
-        if multi:
-            return False
+        """cnmf_als_fit_tol's plan serves this shard (the persistent shape with >= 5 tiles per wave;
+        multi: the exchange form, tests/test_gpu_als.py::test_persistent_als_two_ranks_device_tol)."""
         with torch.cuda.device(self.device):
             probe = self.lib.cnmf_als_persist_workgroups(self.n_rows, self.F, self.k, self.xdt,
                                                          (1 if multi else 0) | 2)

@@ -241,25 +241,71 @@ def test_persistent_als_self_exchange_is_bit_identical():
         dist.destroy_process_group()
 
 
-def _als_rank_main(rank, world, port, N, q):
+def _als_rank_main(rank, world, port, N, q, tol=0.0):
     try:
         import torch
         import torch.distributed as dist
+        from cnmf_amd.solver import run_mu
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         X, W0, H0 = _data(N, 81, 4, seed=21)
         lo, hi = rank * N // world, (rank + 1) * N // world
         plan = _als_plan_group(X[lo:hi].copy(), W0[lo:hi].copy(), H0, 1.0, 0.5, dist.group.WORLD)
         plan.enable_exchange()
-        plan.iterate(9)
-        plan.iterate(11)
+        if tol > 0:  # the exchange-plus-tolerance launch: ONE launch, the test on the all-reduced loss
+            import warnings
+            assert plan._tol_served(True)
+            with warnings.catch_warnings(record=True) as rec:
+                warnings.simplefilter("always")
+                n = run_mu(plan, max_iter=300, tol=tol)
+            assert not rec, [str(r.message) for r in rec]  # the device launch ran, no fallback
+        else:
+            plan.iterate(9)
+            plan.iterate(11)
+            n = 20
         plan.check_sync_error()
-        q.put((rank, plan.W.cpu().numpy(), plan.H64.cpu().numpy(), None))
+        q.put((rank, plan.W.cpu().numpy(), plan.H64.cpu().numpy(), n if tol > 0 else None))
         dist.barrier()
         plan.release()
         dist.destroy_process_group()
     except Exception as ex:  # reported to the parent
         q.put((rank, None, None, f"{type(ex).__name__}: {ex}"))
+
+
+@pytest.mark.timeout(600)
+def test_persistent_als_two_ranks_device_tol():
+    """The exchange-plus-tolerance ALS launch (cnmf_als_fit_tol with xctl): two processes on one GPU,
+    the loss column all-reduced with [WᵀX | WᵀW], the stop decided on it by every rank's top: the
+    oracle's n_iter, the same H on both ranks, W / H at 1e-5."""
+    import multiprocessing as mp
+    world, N = 2, 2 * 16 * 600
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_als_rank_main, args=(r, world, port, N, q, 1e-3)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, W, H, n = q.get(timeout=400)
+            out[r] = (W, H, n)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    bad = [v[2] for v in out.values() if isinstance(v[2], str)]
+    assert not bad, bad
+    assert out[0][2] == out[1][2]
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    W = np.concatenate([out[0][0], out[1][0]])
+    X, W0, H0 = _data(N, 81, 4, seed=21)
+    Wr, Hr, nr = als_ref.als_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                                 max_iter=300, tol=1e-3, sum_to_one=1.0, smoothness=0.5, w_step="enumerate")
+    print(f"two ranks, device tol: n_iter {out[0][2]} (oracle {nr})")
+    assert out[0][2] == nr, (out[0][2], nr)
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(out[0][1], Hr) <= 1e-5, (rel_fro(W, Wr), rel_fro(out[0][1], Hr))
 
 
 @pytest.mark.timeout(600)

@@ -10,12 +10,24 @@ GB/s vs peak, V = 1e6 x 81, k = 4, at 1/2/4/8 GPUs; configs[1] = cfg2 at one GPU
 
 One "step" = one MU iteration (sample pass over X + cross-workgroup reduction + basis update) on
 synthetic IOP spectra (cnmf_amd.synthetic), fp32, tol = 0, inputs resident in HBM before the timed
-region.  Default --scaling weak (the task's rule for a path that shards its units: every rank owns
---rows = 1e6 rows of the sample axis, and the k(F+k) fp64 accumulators — the path's one exchange —
-are all-reduced every iteration, inside the persistent launch over xGMI when validated, else RCCL):
-value = the 1e6-row MU iterations all ranks completed per second (N x rows / 1e6 x K / time;
-exactly cfg2's it/s at N = 1).  --scaling strong: V = --rows x 81 is ONE problem whose rows are
-split over the N ranks in 64-row-aligned shards, value = iterations per second of that problem.
+region.
+
+Default --scaling weak (the task's rule for a path that shards its units): every rank owns --rows
+rows of the sample axis (rank 0's rows are exactly cfg2's X), and the k(F+k) fp64 accumulators —
+the path's one exchange — are all-reduced every iteration, inside the persistent launch over xGMI
+when validated, else RCCL.  value = ranks x K / time in the unit "<rows>-row it/s" (cfg2: "1e6-row
+it/s"): the iterations of one <rows>-row shard that all ranks completed per second (at N = 1 exactly
+the it/s of the problem run).  --scaling strong: V = --rows x 81 is ONE problem (cfg2's X, or
+cfg3's) split over the N ranks in 64-row-aligned shards, value = iterations/s of that problem
+(unit "it/s").
+
+At N > 1 the line also carries `strong`: the metric's own V = --strong-rows (default 1e6) x 81
+problem — cfg2's X and start, split over the same ranks — timed in the same run, and the same
+problem on rank 0's GPU alone, so `strong.speedup_vs_n1` is north_star's strong-scaling figure
+measured on one clock.  At N = 1 `strong` is the line itself.
+
+The bench refuses to report a broken run: a non-finite final error, or a non-finite or negative
+entry of W or H on any rank, exits with status 3 and prints no line.
 
 Extra keys: roofline (the dominant kernel timed with HIP events on its launch stream inside the
 timed region: at N = 1 the ONE persistent launch that runs all K iterations, else each per-iteration
@@ -27,6 +39,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -37,11 +50,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+EXIT_BROKEN = 3  # a run whose final state is not a valid factorisation: no line is printed
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (one rank each); default: WORLD_SIZE when a launcher set it, else 1")
     p.add_argument("--steps", type=int, default=500)
     # 1000 warmup iterations (~70 ms at cfg2): after idle the chip runs its first ~35 ms of work at
     # lower clocks (tools/bench_trend.py: 73.7 us/iteration on the first 500-iteration launch,
@@ -50,9 +65,12 @@ def parse():
     p.add_argument("--rows", type=int, default=1_000_000,
                    help="rows of V: the whole problem (--scaling strong) or per GPU (--scaling weak)")
     p.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                   help="weak (default): every GPU owns --rows rows (V = 1e6 x 81 per GPU), value = "
-                        "1e6-row iterations/s summed over the GPUs; strong: --rows is ONE problem split "
-                        "over the GPUs, value = iterations/s of that problem")
+                   help="weak (default): every GPU owns --rows rows, value = ranks x iterations/s in "
+                        "'<rows>-row it/s'; strong: --rows is ONE problem split over the GPUs, value = "
+                        "iterations/s of that problem")
+    p.add_argument("--strong-rows", type=int, default=1_000_000,
+                   help="at N > 1: also time this V (x F) as ONE problem split over the ranks, and on "
+                        "rank 0's GPU alone (the line's `strong` key); 0 = skip")
     p.add_argument("--features", type=int, default=81)
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
@@ -94,7 +112,7 @@ def parse():
                         "gloo (host-side collectives: lets two ranks share one GPU, as the N > 1 tests do)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                    help="PMC traffic summary written by tools/pmc_traffic.py (optional)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 def cpu_model() -> str:
@@ -214,10 +232,10 @@ def validate_exchange(plan, W0, H0d, n=20):
     plan.iterate(n)  # shard steps + RCCL all_reduce
     torch.cuda.synchronize()
     dH = float((Hx - plan.H64).norm() / plan.H64.norm())
-    dW = float((Wx.double() - plan.W.double()).norm() / plan.W.double().norm())
+    dW = float((Wx.double() - plan.W.double()).norm() / max(float(plan.W.double().norm()), 1e-300))
     hmax, hmin = Hx.clone(), Hx.clone()
-    dist.all_reduce(hmax, op=dist.ReduceOp.MAX)
-    dist.all_reduce(hmin, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hmax, op=dist.ReduceOp.MAX, group=plan.group)
+    dist.all_reduce(hmin, op=dist.ReduceOp.MIN, group=plan.group)
     same = bool(torch.equal(hmax, hmin))
     # the two paths may run different kernels (the exchange: the persistent launch; RCCL: one
     # shard-step launch per iteration), whose fp32 partial sums are grouped differently: agreement
@@ -227,7 +245,7 @@ def validate_exchange(plan, W0, H0d, n=20):
     bar = 1e-6 if type(plan).__name__ == "MUPlan" else 1e-5
     bad = fail or (not same) or not (dH < bar and dW < bar)
     st = torch.tensor([1.0 if bad else 0.0, dH, dW], dtype=torch.float64, device=dev)
-    dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    dist.all_reduce(st, op=dist.ReduceOp.MAX, group=plan.group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
     torch.cuda.synchronize()
@@ -302,19 +320,20 @@ def load_traffic(path, n_rows, F, k):
     return per_it, ent.get("source")
 
 
-def launcher_decision(gpus: int, env, device_count: int, backend: str):
+def launcher_decision(gpus, env, device_count: int, backend: str):
     """How `bench.py --gpus N` runs (never time one rank and call it N):
     ("run", None) — this process is a rank of a world of exactly N (a launcher set WORLD_SIZE = N, or
-    N = 1 without one); ("spawn", None) — no launcher and N > 1: start N ranks as children through
-    torch.distributed.run; ("refuse", why) — WORLD_SIZE disagrees with --gpus, or RCCL would need
-    more devices than are visible."""
+    N = 1 without one; --gpus omitted: whatever WORLD_SIZE the launcher set); ("spawn",
+    None) — no launcher and N > 1: start N ranks as children through torch.distributed.run;
+    ("refuse", why) — WORLD_SIZE disagrees with --gpus, or RCCL would need more devices than are
+    visible."""
     ws = env.get("WORLD_SIZE")
     if ws is not None:
-        if int(ws) != gpus:
+        if gpus is not None and int(ws) != gpus:
             return "refuse", (f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks: the line would "
                               f"report the wrong GPU count")
         return "run", None
-    if gpus <= 1:
+    if gpus is None or gpus <= 1:
         return "run", None
     if backend == "nccl" and device_count < gpus:
         return "refuse", (f"--gpus {gpus} needs {gpus} visible devices for RCCL, {device_count} visible "
@@ -336,79 +355,128 @@ def spawn_ranks(gpus: int) -> int:
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
-def main():
-    args = parse()
+def state_problem(err, W, H) -> str | None:
+    """Why the measured state is not a valid factorisation (None when it is): the final Frobenius
+    error must be finite, and W / H finite and non-negative (a NaN-producing
+    kernel variant was once timed and reported with exit status 0).  W, H: torch tensors or arrays."""
     import torch
-    # decided before any HIP call (device_count does not initialise the runtime on this image)
-    how, why = launcher_decision(args.gpus, os.environ, torch.cuda.device_count(), args.backend)
-    if how == "refuse":
-        print(f"[bench] refused: {why}", file=sys.stderr, flush=True)
-        sys.exit(2)
-    if how == "spawn":
-        sys.exit(spawn_ranks(args.gpus))
-    import torch.distributed as dist
+    if err is None or not math.isfinite(float(err)):
+        return f"final Frobenius error is {err}"
+    for name, t in (("W", W), ("H", H)):
+        t = torch.as_tensor(t)
+        if t.numel() == 0:
+            continue
+        if not bool(torch.isfinite(t).all()):
+            return f"{name} has a non-finite entry"
+        if bool((t < 0).any()):
+            return f"{name} has a negative entry"
+    return None
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.dist and world == 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
-        os.environ.setdefault("RANK", "0")
-        os.environ.setdefault("WORLD_SIZE", "1")
-    dist_path = world > 1 or args.dist
-    # one GPU per rank; with --backend gloo several ranks may share a GPU (local % device count)
-    local_dev = local % max(torch.cuda.device_count(), 1)
-    if dist_path:
-        torch.cuda.set_device(local_dev)
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
-        else:
-            dist.init_process_group("gloo")
-    dev = torch.device("cuda", local_dev)
-    torch.cuda.set_device(dev)
-    group = dist.group.WORLD if dist_path else None
 
-    from cnmf_amd.solver import ALSPlan, MUPlan, WeightedMUPlan
+def final_verdict(plan, world: int, dev):
+    """(final error, problem or None) of the plan's measured state, agreed over the ranks: when any
+    rank's state is not a valid factorisation every rank gets a problem (and refuses together)."""
+    err = plan.frobenius_error()
+    problem = state_problem(err, plan.W, plan.H64)
+    if any_rank(problem is not None, world, dev):
+        problem = problem or "another rank's state is not a valid factorisation"
+    return err, problem
+
+
+def refuse_result(why: str, rank: int):
+    """Exit with EXIT_BROKEN and no JSON line (every rank calls it together)."""
+    print(f"[bench] rank {rank}: refusing to report: {why}", file=sys.stderr, flush=True)
+    sys.exit(EXIT_BROKEN)
+
+
+def row_unit(n_rows: int) -> str:
+    """Label of the weak-scaling unit: the rows of one shard ('1e6' for cfg2's 1,000,000)."""
+    m = math.log10(n_rows) if n_rows > 0 else 0.0
+    if n_rows > 0 and abs(m - round(m)) < 1e-12:
+        return f"1e{int(round(m))}"
+    return str(n_rows)
+
+
+def line_value(scaling: str, world: int, n_rows: int, k_done: int, elapsed: float):
+    """(value, unit) of the JSON line.  weak: world x k_done / elapsed in '<rows>-row it/s' — the
+    iterations of one <rows>-row shard completed per second over all ranks (at N = 1 the it/s of the
+    problem run; ADVICE r4: no rescaling by rows / 1e6); strong: k_done / elapsed in it/s of the
+    whole problem."""
+    if scaling == "strong":
+        return k_done / elapsed, "it/s"
+    return world * k_done / elapsed, f"{row_unit(n_rows)}-row it/s"
+
+
+class Ctx:
+    """Where a measurement runs: this process's rank in a world (group None at world 1)."""
+
+    def __init__(self, world, rank, dev, group, dist_path, backend):
+        self.world, self.rank, self.dev, self.group = world, rank, dev, group
+        self.dist_path, self.backend = dist_path, backend
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.barrier(group=self.group)
+
+
+def make_problem(args, rows_total: int, lo: int, hi: int, seed: int):
+    """Host arrays of rows [lo, hi) of the seeded synthetic problem with rows_total rows (X, W0, H0,
+    weights or None).  Rows are drawn for the whole problem, so any split of it sees the same X."""
     from cnmf_amd.synthetic import iop_spectra, random_init
-
-    F, k = args.features, args.k
-    if args.scaling == "strong":  # the fixed problem, 64-row-aligned shards (persistent tiles)
-        from cnmf_amd.distributed import shard_bounds
-        lo, hi = shard_bounds(args.rows, world, rank, align=64)
-        n_rows = hi - lo
-    else:
-        n_rows = args.rows
     np_dt = np.float64 if args.dtype == "f64" else np.float32
-    # synthetic spectra per shard (seed = rank: at N = 1 exactly cfg2's X); H0 is rank 0's
-    X = iop_spectra(n_rows, F, seed=rank, dtype=np_dt)
-    W0, H0 = random_init(X, k, 42 + rank)
+    X = iop_spectra(rows_total, args.features, seed=seed, dtype=np_dt)
+    W0, H0 = random_init(X, args.k, 42 + seed)
+    Mw = None
+    if args.weighted:
+        rng = np.random.default_rng(seed)
+        Mw = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)[lo:hi]
+    if lo != 0 or hi != rows_total:
+        X, W0 = np.ascontiguousarray(X[lo:hi]), np.ascontiguousarray(W0[lo:hi])
+    return X, W0, H0, Mw
+
+
+def make_plan(args, ctx, X, W0, H0, Mw, Xd=None):
+    """The plan of one measurement on ctx's device (X copied to HBM unless Xd is given); H0 is
+    broadcast from rank 0.  Returns (plan, Xt host tensor, H0 on the device)."""
+    import torch
+    import torch.distributed as dist
+    from cnmf_amd.solver import ALSPlan, MUPlan, WeightedMUPlan
     Xt = torch.from_numpy(X)
     if args.dtype == "bf16":
         Xt = Xt.to(torch.bfloat16)
-    Xd = Xt.to(dev)
-    H0d = torch.from_numpy(H0).to(dev)
-    if world > 1:
-        dist.broadcast(H0d, src=0)
+    if Xd is None:
+        Xd = Xt.to(ctx.dev)
+    H0d = torch.from_numpy(H0).to(ctx.dev)
+    if ctx.world > 1:
+        dist.broadcast(H0d, src=0, group=ctx.group)
     if args.weighted:
-        rng = np.random.default_rng(rank)
-        Mw = (rng.uniform(0.2, 2.0, X.shape) * (rng.random(X.shape) >= 0.3)).astype(np.float32)
-        plan = WeightedMUPlan(Xd, torch.from_numpy(Mw).to(dev), k, group=group)
+        plan = WeightedMUPlan(Xd, torch.from_numpy(Mw).to(ctx.dev), args.k, group=ctx.group)
     elif args.solver == "als":
-        plan = ALSPlan(Xd, k, sum_to_one=args.sum_to_one, smoothness=args.smoothness, group=group)
+        plan = ALSPlan(Xd, args.k, sum_to_one=args.sum_to_one, smoothness=args.smoothness, group=ctx.group)
     else:
-        plan = MUPlan(Xd, k, group=group)
+        plan = MUPlan(Xd, args.k, group=ctx.group)
     plan.set_W(torch.from_numpy(W0))
     plan.set_H(H0d)
+    return plan, Xt, H0d
+
+
+def measure(args, ctx, plan, W0, H0d, K, warmup, ramp_seconds, tune=True):
+    """Warm up, ramp the clock, tune the layout, then time exactly K steps of `plan` bracketed by a
+    barrier + synchronisation on both sides (max over ranks).  Returns a dict of the timing, the
+    paths taken and the measured state's verdict (`problem`, agreed over the ranks)."""
+    import torch
+    from cnmf_amd.solver import agree_max
+    world, rank, dev = ctx.world, ctx.rank, ctx.dev
     exchange = None
-    if dist_path and args.exchange == "auto" and plan.exchange_shape:
+    if ctx.dist_path and args.exchange == "auto" and plan.exchange_shape:
         exchange = validate_exchange(plan, W0, H0d)
-        print(f"[rank {rank}] in-launch exchange: {exchange}", file=sys.stderr, flush=True)
+        print(f"[rank {rank}] in-launch exchange ({plan.n_rows} rows): {exchange}", file=sys.stderr, flush=True)
     elif args.dist and args.solver == "mu" and not args.weighted:
         plan.use_shard_steps()
     torch.cuda.synchronize()
 
-    plan.iterate(args.warmup)
+    plan.iterate(warmup)
     torch.cuda.synchronize()
     if getattr(plan, "exchange", False):  # a failed warmup launch falls back before anything is timed
         fail = False
@@ -422,15 +490,15 @@ def main():
             exchange = "failed in warmup; RCCL path timed"
             plan.set_W(torch.from_numpy(W0))
             plan.set_H(H0d)
-            plan.iterate(args.warmup)
+            plan.iterate(warmup)
             torch.cuda.synchronize()
 
     # clock ramp: after idle the chip runs its first tens of ms of work at lower clocks (r01/r02:
     # a 20-step timing after a 5-step warmup read 66 us per iteration against 57-58 us once warm);
     # run untimed iterations on copies of W / H until ramp_s of GPU time has passed
     ramp_s, ramp_trips = 0.0, 0
-    if args.ramp_seconds > 0:
-        ramp_s, ramp_trips = clock_ramp(plan, args.ramp_seconds, world, dev, torch.cuda.synchronize)
+    if ramp_seconds > 0:
+        ramp_s, ramp_trips = clock_ramp(plan, ramp_seconds, world, dev, torch.cuda.synchronize)
         plan.check_sync_error()
 
     # the persistent launch has several layouts whose order can differ between boxes: time them on
@@ -440,18 +508,15 @@ def main():
     tuned = {}
     if args.layout > 0 and args.solver == "mu" and not args.weighted:
         plan.set_layout(args.layout)
-    elif args.solver == "mu" and getattr(plan, "layouts", ()) and not args.no_tune and not args.weighted:
+    elif tune and args.solver == "mu" and getattr(plan, "layouts", ()) and not args.no_tune and not args.weighted:
         tuned = plan.tune(n_iter=100, rounds=2)
         print(f"[rank {rank}] persistent layouts (us/iteration): {tuned}", file=sys.stderr, flush=True)
     layout = plan.describe() if plan.persistent else None
     layouts = [getattr(plan, "layout", None)]
     if world > 1:
+        import torch.distributed as dist
         layouts = [None] * world
-        dist.all_gather_object(layouts, getattr(plan, "layout", None))
-    if layout and "floating" in layout:
-        layout += " (80 % resident, 20 % drawn from a pool every iteration)"
-
-    K = args.steps
+        dist.all_gather_object(layouts, getattr(plan, "layout", None), group=ctx.group)
 
     tol_result = {}
 
@@ -481,14 +546,12 @@ def main():
         torch.cuda.synchronize()
         if args.settle_ms > 0:
             time.sleep(args.settle_ms / 1e3)
-        if world > 1:
-            dist.barrier()
+        ctx.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run()
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        ctx.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
         return persistent, events, elapsed, whole
@@ -506,7 +569,7 @@ def main():
             exchange = "failed in the timed launch; RCCL path re-timed"
             plan.set_W(torch.from_numpy(W0))
             plan.set_H(H0d)
-            plan.iterate(args.warmup)
+            plan.iterate(warmup)
             torch.cuda.synchronize()
             persistent, events, elapsed, whole = timed()
     plan.check_sync_error()
@@ -520,26 +583,140 @@ def main():
         launches = K
         avg_launch_s = float(np.mean([events[2 * i].elapsed_time(events[2 * i + 1])
                                       for i in range(K)])) / 1e3
-    avg_pass_s = avg_launch_s
+    elapsed, avg_launch_s_max = agree_max([elapsed, avg_launch_s], ctx.group if world > 1 else None, dev)
 
-    from cnmf_amd.solver import agree_max
-    elapsed, avg_pass_s_max = agree_max([elapsed, avg_pass_s], dist.group.WORLD if world > 1 else None, dev)
+    err, problem = final_verdict(plan, world, dev)
+    return {"persistent": persistent, "whole": whole, "elapsed": elapsed, "avg_launch_s": avg_launch_s,
+            "avg_launch_s_max": avg_launch_s_max, "launches": launches, "exchange": exchange,
+            "layout": layout, "layouts": layouts, "tuned": tuned, "ramp_s": ramp_s,
+            "ramp_trips": ramp_trips, "tol_result": tol_result, "err": err, "problem": problem,
+            "k_done": tol_result.get("n_iter", K)}
 
+
+def bytes_per_iteration(args, n_rows: int) -> int:
+    """Algorithmic HBM bytes of one pass over n_rows: X once, W read and written
+    (+ the weights for the weighted MU)."""
     sx = {"f32": 4, "f64": 8, "bf16": 2}[args.dtype]
     sw = 8 if args.dtype == "f64" else 4
-    bytes_per_pass = n_rows * (F * sx + 2 * k * sw) + (n_rows * F * 4 if args.weighted else 0)  # + M
-    iters_per_launch = tol_result.get("n_iter", K) if persistent else 1
-    bytes_per_launch = bytes_per_pass * iters_per_launch
-    achieved = bytes_per_launch / avg_pass_s_max / 1e9
+    return n_rows * (args.features * sx + 2 * args.k * sw) + (n_rows * args.features * 4 if args.weighted else 0)
 
-    # sanity of the measured state (cheap): the objective is finite, W/H non-negative
-    err = plan.frobenius_error()
+
+def strong_block(args, res, n_rows_shard: int, rows: int, world: int, n1=None):
+    """The line's `strong` key: the fixed rows x F problem over `world` ranks (res) and on one GPU
+    (n1: the same problem on rank 0's GPU alone, in the same run; at N = 1 res itself)."""
+    us = res["elapsed"] / res["k_done"] * 1e6
+    per_launch = res["avg_launch_s_max"] / (res["k_done"] if res["persistent"] else 1)
+    frac = bytes_per_iteration(args, n_rows_shard) / per_launch / 1e9 / HBM_PEAK_GBS
+    out = {"rows": rows, "ranks": world, "rows_per_gpu_max": n_rows_shard,
+           "it_s": round(res["k_done"] / res["elapsed"], 2), "us_per_iteration": round(us, 3),
+           "frac": round(frac, 4), "exchange": res["exchange"],
+           "layout": res["layout"]}
+    if n1 is not None:
+        us1 = n1["elapsed"] / n1["k_done"] * 1e6
+        out["n1_it_s"] = round(n1["k_done"] / n1["elapsed"], 2)
+        out["n1_us_per_iteration"] = round(us1, 3)
+        out["speedup_vs_n1"] = round(us1 / us, 3)
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    # decided before any HIP call (device_count does not initialise the runtime on this image)
+    how, why = launcher_decision(args.gpus, os.environ, torch.cuda.device_count(), args.backend)
+    if how == "refuse":
+        print(f"[bench] refused: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if how == "spawn":
+        sys.exit(spawn_ranks(args.gpus))
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dist and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    dist_path = world > 1 or args.dist
+    # one GPU per rank; with --backend gloo several ranks may share a GPU (local % device count)
+    n_dev = max(torch.cuda.device_count(), 1)
+    local_dev = local % n_dev
+    if dist_path:
+        torch.cuda.set_device(local_dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_dev))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", local_dev)
+    torch.cuda.set_device(dev)
+    ctx = Ctx(world, rank, dev, dist.group.WORLD if dist_path else None, dist_path, args.backend)
+
+    from cnmf_amd.distributed import shard_bounds
+
+    F, k, K = args.features, args.k, args.steps
+    if args.scaling == "strong":  # the fixed problem (cfg2's X), 64-row-aligned shards (persistent tiles)
+        lo, hi = shard_bounds(args.rows, world, rank, align=64)
+        X, W0, H0, Mw = make_problem(args, args.rows, lo, hi, seed=0)
+    else:  # every rank its own rows (seed = rank: rank 0's are exactly cfg2's X)
+        X, W0, H0, Mw = make_problem(args, args.rows, 0, args.rows, seed=rank)
+    n_rows = X.shape[0]
+    plan, Xt, H0d = make_plan(args, ctx, X, W0, H0, Mw)
+    res = measure(args, ctx, plan, W0, H0d, K, args.warmup, args.ramp_seconds)
+    if res["problem"]:
+        refuse_result(res["problem"], rank)
+
+    # north_star's strong-scaling figure on one clock: the metric's V = strong_rows problem split over
+    # the same ranks, and on rank 0's GPU alone (ranks > 0 wait at the barrier meanwhile)
+    strong = None
+    S = args.strong_rows
+    if world > 1 and S > 0:
+        if args.scaling == "strong" and S == args.rows:
+            sres, s_rows, s_plan = res, n_rows, None
+        else:
+            slo, shi = shard_bounds(S, world, rank, align=64)
+            Xs, W0s, H0s, Mws = make_problem(args, S, slo, shi, seed=0)
+            s_plan, _, H0sd = make_plan(args, ctx, Xs, W0s, H0s, Mws)
+            sres = measure(args, ctx, s_plan, W0s, H0sd, K, min(args.warmup, 200), 0.1)
+            s_rows = Xs.shape[0]
+            if sres["problem"]:
+                refuse_result("strong split: " + sres["problem"], rank)
+        s_rows_max = int(max(shard_bounds(S, world, r, align=64)[1] - shard_bounds(S, world, r, align=64)[0]
+                             for r in range(world)))
+        n1 = None
+        if s_plan is not None:
+            s_plan.release()
+        if rank == 0:
+            ctx1 = Ctx(1, 0, dev, None, False, args.backend)
+            X1, W01, H01, Mw1 = make_problem(args, S, 0, S, seed=0)
+            p1, _, H01d = make_plan(args, ctx1, X1, W01, H01, Mw1)
+            n1 = measure(args, ctx1, p1, W01, H01d, K, min(args.warmup, 200), 0.1)
+            del p1
+        n1_bad = rank == 0 and n1["problem"] is not None
+        if any_rank(n1_bad, world, dev):
+            refuse_result("one-GPU reference of the strong split: " + (n1["problem"] if n1_bad else "rank 0"), rank)
+        if rank == 0:
+            strong = strong_block(args, sres, s_rows_max, S, world, n1)
+    elif world == 1 and S > 0 and n_rows == S and not args.dist:
+        strong = strong_block(args, res, n_rows, S, 1)
+        strong["n1_it_s"], strong["n1_us_per_iteration"], strong["speedup_vs_n1"] = (
+            strong["it_s"], strong["us_per_iteration"], 1.0)
 
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
+
+    persistent = res["persistent"]
+    tol_result = res["tol_result"]
+    elapsed, avg_pass_s, avg_pass_s_max = res["elapsed"], res["avg_launch_s"], res["avg_launch_s_max"]
+    bytes_per_pass = bytes_per_iteration(args, n_rows)
+    iters_per_launch = tol_result.get("n_iter", K) if persistent else 1
+    bytes_per_launch = bytes_per_pass * iters_per_launch
+    achieved = bytes_per_launch / avg_pass_s_max / 1e9
+    layout = res["layout"]
 
     traffic, traffic_src = (None, None) if (args.solver == "als" or args.weighted) else load_traffic(args.traffic_json, n_rows, F, k)
     if traffic is not None:
@@ -573,7 +750,7 @@ def main():
                 "traffic": traffic, "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "algorithmic_bytes_per_iteration": bytes_per_pass,
-                "launches_timed": launches, "iterations_per_launch": iters_per_launch,
+                "launches_timed": res["launches"], "iterations_per_launch": iters_per_launch,
                 "avg_launch_us": round(avg_pass_s * 1e6, 2),
                 "avg_us_per_iteration_in_launch": round(avg_pass_s / iters_per_launch * 1e6, 2),
                 "max_over_ranks_avg_launch_us": round(avg_pass_s_max * 1e6, 2)}
@@ -586,11 +763,9 @@ def main():
         else:
             cpu = cpu_baseline(Xc, W0, H0, args.cpu_seconds)
 
-    K_done = tol_result.get("n_iter", K)  # --tol: the iterations the fit actually ran
-    if args.scaling == "strong":
-        value = K_done / elapsed  # iterations per second of the whole (fixed) problem
-    else:
-        value = world * n_rows / 1e6 * K_done / elapsed
+    K_done = res["k_done"]  # --tol: the iterations the fit actually ran
+    value, unit = line_value(args.scaling, world, n_rows, K_done, elapsed)
+    n_rows_total = args.rows if args.scaling == "strong" else world * n_rows
     if args.weighted:
         metric = "weighted MU iterations/sec (V=1e6x81 k=4 with per-element weights, 30 % zero)"
         workload = (f"weighted / masked MU (SURVEY 8f row 2, tol=0) on V={n_rows}x{F} per GPU, k={k}, "
@@ -605,51 +780,54 @@ def main():
         cfg = {(1_000_000, 81, 4, "f32"): "cfg2", (10_000_000, 81, 8, "f32"): "cfg3",
                (1_250_000, 81, 8, "f32"): "cfg3 (one GPU's shard)",
                (1_000_000, 300, 16, "bf16"): "cfg4"}.get((args.rows, F, k, args.dtype), "custom")
+        metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6×81 k=4, 1/2/4/8 GPU"
+                  if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
         if args.scaling == "strong":
-            metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6\u00d781 k=4, 1/2/4/8 GPU"
-                      if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
             workload = (f"{cfg}: MU (Frobenius, tol={args.tol:g}) on V={args.rows}x{F} in total, k={k}, "
                         f"{args.dtype} synthetic IOP spectra, rows split over {world} GPU(s) in "
-                        f"64-row-aligned shards (strong scaling: the problem is fixed)")
+                        f"64-row-aligned shards (strong scaling: the problem is fixed; value = its it/s)")
         else:
-            metric = ("MU iterations/sec & achieved HBM GB/s vs peak, V=1e6\u00d781 k=4, 1/2/4/8 GPU"
-                      if cfg == "cfg2" else f"MU iterations/sec & achieved HBM GB/s vs peak, {cfg}")
             workload = (f"{cfg}: MU (Frobenius, tol={args.tol:g}) on V={n_rows}x{F} per GPU, k={k}, "
                         f"{args.dtype} synthetic IOP spectra (weak scaling: every GPU owns its own "
                         f"{n_rows} rows of one {world * n_rows}-row problem, [WᵀX | WᵀW] all-reduced "
-                        f"every iteration; value = {n_rows / 1e6:g}e6-row iterations/s summed over "
-                        f"the {world} GPU(s))")
+                        f"every iteration; value = {world} x the it/s of that problem = iterations of "
+                        f"one {n_rows}-row shard per second over all ranks)")
+    # ranks that share a device (--backend gloo on fewer GPUs) are not more GPUs
+    n_gpus = min(world, n_dev) if args.backend == "gloo" and dist_path else world
     out = {
         "metric": metric,
         "value": round(value, 2),
-        "unit": "it/s",
-        "n_gpus": world,
+        "unit": unit,
+        "n_gpus": n_gpus,
+        "ranks": world,
         "steps": K,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / max(tol_result.get("n_iter", K), 1) * 1e3, 4),
+        "ms_per_step": round(elapsed / max(K_done, 1) * 1e3, 4),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f64": "f64", "bf16": "bf16 X / f32 W"}[args.dtype],
         "data": "synthetic",
         "config": {"workload": workload,
-                   "n_rows_total": args.rows if args.scaling == "strong" else world * n_rows,
+                   "n_rows_total": n_rows_total,
                    "n_rows_per_gpu": n_rows, "n_features": F, "k": k,
                    "parallelism": f"dp{world} (row shards, all_reduce of k(F+k) fp64"
                                   + (", in-launch over xGMI)" if plan.exchange else ", RCCL)")
-                                  + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else ""),
-                   "exchange": exchange,
+                                  + (" [--dist: multi-GPU path at one rank]" if args.dist and world == 1 else "")
+                                  + (f" [{world} ranks on {n_gpus} GPU(s): diagnostic]" if n_gpus < world else ""),
+                   "exchange": res["exchange"],
                    "persistent_layout": layout if plan.persistent else None,
-                   "layout_per_rank": layouts,
+                   "layout_per_rank": res["layouts"],
                    "backend": (args.backend if dist_path else None),
-                   "layout_tuning_us_per_iteration": {str(k): round(v, 2) for k, v in tuned.items()} or None,
-                   "clock_ramp_s": round(ramp_s, 3), "clock_ramp_trips": ramp_trips,
+                   "layout_tuning_us_per_iteration": {str(kk): round(v, 2) for kk, v in res["tuned"].items()} or None,
+                   "clock_ramp_s": round(res["ramp_s"], 3), "clock_ramp_trips": res["ramp_trips"],
                    "tol": args.tol or None,
                    "tol_n_iter": tol_result.get("n_iter"),
                    "tol_errors": tol_result.get("errors")},
         "roofline": roofline,
+        "strong": strong,
         "cpu_baseline": cpu,
-        "final_frobenius_error": err,
+        "final_frobenius_error": res["err"],
     }
     print(json.dumps(out), flush=True)
     if world > 1:

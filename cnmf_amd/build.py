@@ -48,6 +48,14 @@ def build(verbose: bool = False, force: bool = False, stamps: bool = False, diag
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    if not stamps and not diag:
+        # the shipped wave-tile kernels' prefetch registers must never be spilled (tools/kcheck.py)
+        chk = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "kcheck.py"), out + ".tmp"],
+                             capture_output=True, text=True)
+        if chk.returncode != 0:
+            os.remove(out + ".tmp")
+            raise RuntimeError("kernel check failed (prefetch registers touched outside their loads):\n"
+                               + chk.stdout[-3000:])
     os.replace(out + ".tmp", out)
     return out
 

@@ -3497,6 +3497,7 @@ __device__ __forceinline__ void wait_n() {
 }
 template <int N, int C>
 __device__ __forceinline__ void wait_set(u32x4 (&pf)[C]) {
+  static_assert(N >= 0 && N <= 63, "s_waitcnt vmcnt is a 6-bit field: a deeper prefetch cannot be counted");
   if constexpr (C == 7)
     asm volatile("s_waitcnt vmcnt(%7)"
                  : "+a"(pf[0]), "+a"(pf[1]), "+a"(pf[2]), "+a"(pf[3]), "+a"(pf[4]), "+a"(pf[5]), "+a"(pf[6])
@@ -3729,6 +3730,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // W keeps that snapshot in LDS: no store, so the counted waits are the plain kernel's)
   constexpr int NSTB = (WRES ? 0 : 1) + (TOL && !WRES ? 1 : 0);
   constexpr int KP = KK / 2;                 // component pairs
+  // the PD prefetch sets live in AGPRs (4 per load) next to the kernel's own registers: past a
+  // budget the allocator spills them to scratch right behind their loads, i.e. before the data has
+  // landed, and the staged tiles are stale (k = 8 streamed W at PD = 6: 96 AGPRs, all-NaN W at 2.5x
+  // the time).  tools/kcheck.py checks the built library for exactly that; the
+  // depths measured clean are allowed here (k = 8: PD <= 5, 80 AGPRs; k = 4: PD <= 4, 96)
+  static_assert(4 * PD * PFS <= (KK == 8 ? 80 : 96), "prefetch depth past the measured AGPR budget");
+  static_assert(PFS * (PD - 1) + NSTB * PD <= 63, "the counted wait's vmcnt is a 6-bit field");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
   const int l = t & 63;
@@ -5028,13 +5036,30 @@ __device__ __forceinline__ void als_hstep_block(unsigned char* smem, int F, int 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 // The same sweep for F <= 128 on ONE wave, without a workgroup barrier inside it (same LDS layout;
-// the other waves wait at the closing barrier).  Lane l holds features l and l + 64 in registers;
-// the passive set is compressed by ballots, and each solve M_PP x = b_P is a parallel cyclic
-// reduction over 2x2 blocks of the compressed pentadiagonal system (log2(n/2) steps of register
-// arithmetic and lane shuffles) instead of the n sequential steps of a banded LDLᵀ, whose
-// loop-carried chain of ~10 dependent fp64 operations made a row cost 20-40 k cycles
-// (profiles/r02/session5/als_diag).  LDS is only used for gathers and neighbour reads, in program
-// order inside the wave.
+// the other waves wait at the closing barrier).  Lane l holds features 2l and 2l + 1 (round 5: the
+// pair layout), so a feature's neighbours f ± 1, f ± 2 are the lane's other feature or one of the
+// two adjacent lanes' pair: the Jacobi sweeps and the dual checks fetch them with wave_shr / wave_shl
+// DPP moves (a few cycles) instead of an LDS store + read round trip per sweep.  (The rows of WᵀX
+// and H are still read from LDS per row: holding all k rows in registers raised the persistent
+// kernel's spills from 26 to 72 VGPRs, where the reads are one batch per row.)  Rows whose Jacobi
+// contraction bound is not small take the block PCR: the passive set compressed by ballots and each
+// solve M_PP x = b_P a parallel cyclic reduction over 2x2 blocks of the compressed pentadiagonal
+// system (log2(n/2) steps of register arithmetic and lane shuffles) instead of the n sequential steps
+// of a banded LDLᵀ, whose loop-carried chain of ~10 dependent fp64 operations made a row cost
+// 20-40 k cycles (profiles/r02/session5/als_diag).  The arithmetic of every value — the same fused
+// operations in the same order, neighbours outside the row entering with zero coefficients — is
+// unchanged from the lane = (f, f + 64) form: the sweep's result is the same bits.
+__device__ __forceinline__ double dpp_wave_shr(double v) {  // lane i <- lane i - 1 (lane 0: 0)
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_wave_shl(double v) {  // lane i <- lane i + 1 (lane 63: 0)
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
 __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k, double lam, int t) {
 #ifdef CNMF_STAMPS
   const unsigned hs_call = blockIdx.x == 0 ? __hip_atomic_load(&g_hs_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 64u;
@@ -5056,7 +5081,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     double ld0[2], le1[2], le2[2], lm1[2], lm2[2];  // lm1/lm2: λ·L[f-1][f], λ·L[f-2][f]
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      const int f = lane + 64 * c;
+      const int f = 2 * lane + c;
       ld0[c] = f < F ? lam * als_L_entry(F, f, f) : 0.0;
       le1[c] = f + 1 < F ? lam * als_L_entry(F, f, f + 1) : 0.0;
       le2[c] = f + 2 < F ? lam * als_L_entry(F, f, f + 2) : 0.0;
@@ -5066,6 +5091,9 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     for (int j = 0; j < k; ++j) {
       const double bjj = sB[j * k + j];
       if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
+      double bjm[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) bjm[m] = m < k ? sB[j * k + m] : 0.0;
 #ifdef CNMF_STAMPS
       const unsigned long long hs_t0 = __builtin_amdgcn_s_memtime();
       int hs_iters = 0;
@@ -5086,18 +5114,20 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       bool pas[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const int f = lane + 64 * c;
+        const int f = 2 * lane + c;
         rb[c] = 0.0; rd[c] = 1.0; re1[c] = 0.0; re2[c] = 0.0; xf[c] = 0.0;
         pas[c] = false;
+        const double hj = f < F ? sH[j * F + f] : 0.0;
         if (f < F) {
           double b = sA[j * F + f];
-          for (int m = 0; m < k; ++m)
-            if (m != j) b -= sB[j * k + m] * sH[m * F + f];
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (m < k && m != j) b -= bjm[m] * sH[m * F + f];
           rb[c] = b;
           rd[c] = bjj + ld0[c];
           re1[c] = le1[c];
           re2[c] = le2[c];
-          pas[c] = sH[j * F + f] > 0.0;
+          pas[c] = hj > 0.0;
           if (!jac) {  // the PCR's gathers read the row from LDS
             vb[f] = rb[c];
             d0[f] = rd[c];
@@ -5105,17 +5135,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
             e2[f] = re2[c];
           }
         }
-      }
-      // neighbour indices clamped into the row (their coefficients are zero there): branch-free
-      // sweeps and checks
-      int fm1[2], fp1[2], fm2[2], fp2[2];
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int f = min(lane + 64 * c, F - 1);
-        fm1[c] = max(f - 1, 0);
-        fm2[c] = max(f - 2, 0);
-        fp1[c] = min(f + 1, F - 1);
-        fp2[c] = min(f + 2, F - 1);
+        xf[c] = pas[c] ? hj : 0.0;  // warm start
       }
       int alpha = 3, beta = F + 1;  // BPP control (wave-uniform)
       // Jacobi: the row's Hessian M = B_jj·I + λ·DᵀD has off-diagonal row sums at most 10λ (the
@@ -5123,50 +5143,45 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // contraction of any passive subsystem M_PP in the max norm.  At ρ <= 1/20 (B_jj is a sum over
       // all samples: ρ ~ 1e-4 at cfg5) sweeps from the warm start x = h_j reach the fp64 fixed
       // point in a few steps (bound: ρ^nsw <= 2^-55, and a sweep that changes no bit ends early) —
-      // the same solve as the block PCR below at a fraction of its per-row cost (two LDS round trips
-      // per sweep instead of six shuffle steps of 2x2 blocks and the passive-set compression).
+      // the same solve as the block PCR below at a fraction of its per-row cost.
       int nsw = 0;
       for (double r = 1.0; jac && r > 0x1p-55; r *= rho) ++nsw;
       double rinv[2] = {1.0 / rd[0], 1.0 / rd[1]};
-#pragma unroll
-      for (int c = 0; c < 2; ++c) xf[c] = pas[c] ? sH[j * F + lane + 64 * c] : 0.0;  // warm start
       HS_MARK(0);
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
        if (jac) {
-        // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P)
+        // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P); the neighbours
+        // x[2l-2], x[2l-1] from lane l - 1 and x[2l+2], x[2l+3] from lane l + 1
         for (int sw = 0; sw < nsw; ++sw) {
-#pragma unroll
-          for (int c = 0; c < 2; ++c)
-            if (lane + 64 * c < F) vx[lane + 64 * c] = xf[c];
-          lds_order();
-          bool chg = false;
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            double r = rb[c];
-            r = fma(-lm1[c], vx[fm1[c]], r);
-            r = fma(-re1[c], vx[fp1[c]], r);
-            r = fma(-lm2[c], vx[fm2[c]], r);
-            r = fma(-re2[c], vx[fp2[c]], r);
-            const double xn = pas[c] ? r * rinv[c] : 0.0;  // (pas is false past F)
-            chg = chg || xn != xf[c];
-            xf[c] = xn;
-          }
-          lds_order();
+          const double p0 = dpp_wave_shr(xf[0]), p1 = dpp_wave_shr(xf[1]);
+          const double n0 = dpp_wave_shl(xf[0]), n1 = dpp_wave_shl(xf[1]);
+          double r0 = rb[0];
+          r0 = fma(-lm1[0], p1, r0);
+          r0 = fma(-re1[0], xf[1], r0);
+          r0 = fma(-lm2[0], p0, r0);
+          r0 = fma(-re2[0], n0, r0);
+          double r1 = rb[1];
+          r1 = fma(-lm1[1], xf[0], r1);
+          r1 = fma(-re1[1], n0, r1);
+          r1 = fma(-lm2[1], p1, r1);
+          r1 = fma(-re2[1], n1, r1);
+          const double x0 = pas[0] ? r0 * rinv[0] : 0.0;  // (pas is false past F)
+          const double x1 = pas[1] ? r1 * rinv[1] : 0.0;
+          const bool chg = (x0 != xf[0]) || (x1 != xf[1]);
+          xf[0] = x0;
+          xf[1] = x1;
           if (!__ballot(chg)) break;
         }
-#pragma unroll
-        for (int c = 0; c < 2; ++c)
-          if (lane + 64 * c < F) vx[lane + 64 * c] = xf[c];
-        lds_order();
         HS_MARK(2);
        } else {
-        // ---- compress the passive set: idx[pos] = feature
+        // ---- compress the passive set in feature order: idx[pos] = feature
         const uint64_t bal0 = __ballot(pas[0]), bal1 = __ballot(pas[1]);
-        const int n0 = __popcll(bal0), n = n0 + __popcll(bal1);
-        const int pos[2] = {(int)__popcll(bal0 & lt), n0 + (int)__popcll(bal1 & lt)};
+        const int n = __popcll(bal0) + __popcll(bal1);
+        const int pos0 = (int)__popcll(bal0 & lt) + (int)__popcll(bal1 & lt);
+        const int pos[2] = {pos0, pos0 + (pas[0] ? 1 : 0)};
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-          if (pas[c]) idx[pos[c]] = lane + 64 * c;
+          if (pas[c]) idx[pos[c]] = 2 * lane + c;
         lds_order();
         // ---- M_PP x = b_P by parallel cyclic reduction on 2x2 blocks (lane i = compressed rows
         // 2i, 2i+1; nb = ceil(n/2) <= 64 blocks; log2(nb) steps instead of n sequential LDLᵀ
@@ -5244,33 +5259,36 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
         lds_order();
         HS_MARK(2);
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int f = lane + 64 * c;
-          xf[c] = pas[c] ? vz[pos[c]] : 0.0;
-          if (f < F) vx[f] = xf[c];
-        }
+        for (int c = 0; c < 2; ++c) xf[c] = pas[c] ? vz[pos[c]] : 0.0;
         lds_order();
        }
+        // the KKT check: x >= 0 on P, the dual y = (M x − b)_f >= 0 off P (neighbours outside the
+        // row enter with zero coefficients)
         bool bad[2];
+        {
+          const double p0 = dpp_wave_shr(xf[0]), p1 = dpp_wave_shr(xf[1]);
+          const double n0 = dpp_wave_shl(xf[0]), n1 = dpp_wave_shl(xf[1]);
+          const double nm1[2] = {p1, xf[0]}, np1[2] = {xf[1], n0}, nm2[2] = {p0, p1}, np2[2] = {n0, n1};
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const int f = lane + 64 * c;
-          bad[c] = false;
-          if (f < F) {
-            const double x = xf[c];
-            // (off P: the dual y = (M x − b)_f, its neighbour terms with the clamped indices
-            // zero-weighted at the row's ends)
-            double y = rd[c] * x - rb[c];
-            y += re1[c] * vx[fp1[c]];
-            y += lm1[c] * vx[fm1[c]];
-            y += re2[c] * vx[fp2[c]];
-            y += lm2[c] * vx[fm2[c]];
-            bad[c] = pas[c] ? x < 0.0 : y < 0.0;
+          for (int c = 0; c < 2; ++c) {
+            const int f = 2 * lane + c;
+            bad[c] = false;
+            if (f < F) {
+              const double x = xf[c];
+              double y = rd[c] * x - rb[c];
+              y += re1[c] * np1[c];
+              y += lm1[c] * nm1[c];
+              y += re2[c] * np2[c];
+              y += lm2[c] * nm2[c];
+              bad[c] = pas[c] ? x < 0.0 : y < 0.0;
+            }
           }
         }
         const uint64_t bb0 = __ballot(bad[0]), bb1 = __ballot(bad[1]);
         const int ninf = __popcll(bb0) + __popcll(bb1);
-        const int maxbad = bb1 ? 64 + 63 - __clzll(bb1) : (bb0 ? 63 - __clzll(bb0) : -1);
+        const int mb0 = bb0 ? 2 * (63 - __clzll(bb0)) : -1;
+        const int mb1 = bb1 ? 2 * (63 - __clzll(bb1)) + 1 : -1;
+        const int maxbad = mb0 > mb1 ? mb0 : mb1;
         int mode;
         if (ninf == 0) mode = 0;
         else if (ninf < beta) { beta = ninf; alpha = 3; mode = 1; }
@@ -5283,12 +5301,13 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
         if (mode == 0) break;
 #pragma unroll
         for (int c = 0; c < 2; ++c)
-          if ((mode == 1 && bad[c]) || (mode == 2 && lane + 64 * c == maxbad)) pas[c] = !pas[c];
+          if ((mode == 1 && bad[c]) || (mode == 2 && 2 * lane + c == maxbad)) pas[c] = !pas[c];
       }
 #undef HS_MARK
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (lane + 64 * c < F) sH[j * F + lane + 64 * c] = fmax(xf[c], 0.0);
+      for (int c = 0; c < 2; ++c) {
+        if (2 * lane + c < F) sH[j * F + 2 * lane + c] = fmax(xf[c], 0.0);
+      }
       lds_order();
 #ifdef CNMF_STAMPS
       if (lane == 0 && hs_call < 64u && j < 4) {
@@ -8964,3 +8983,11 @@ int cnmf_init_fill(const double* U, int64_t n_rows, int k, const double* coef, c
   return CNMF_OK;
 }
 }  // extern "C"
+
+#ifdef CNMF_PD_PROBE
+// diagnostic (tools/audit_wt_asm.py): the k = 8 streamed-W wave-tile kernel at a
+// prefetch depth the product never launches, compiled only to inspect its ISA
+namespace cnmf {
+template __global__ void mu_iter_wt_kernel<8, false, CNMF_PD_PROBE, false, false>(PersistArgs);
+}
+#endif

@@ -421,11 +421,25 @@ class MUPlan:
                     *_event_array(pass_events), self._stream()), "cnmf_mu_iterations_multi")
             return
         if self.world == 1 and not self.shard_steps and self.persistent_shape and not self.persistent:
-            # kept off the persistent kernel (a launch of it failed): pass + reduce + update launches
-            for _ in range(n_iter):
+            # kept off the persistent kernel (a launch of it failed): pass + reduce + update launches;
+            # pass_events as documented (unrecorded events read ~0 s and an absurd rate)
+            ev = list(pass_events) if pass_events is not None else None
+            stream = torch.cuda.current_stream(self.device) if ev is not None else None
+            whole = ev is not None and len(ev) == 2
+            if ev is not None and not whole and len(ev) != 2 * n_iter:
+                raise ValueError(f"pass_events: 2 or 2*n_iter events, got {len(ev)}")
+            if whole:
+                ev[0].record(stream)
+            for i in range(n_iter):
+                if ev is not None and not whole:
+                    ev[2 * i].record(stream)
                 self.sample_pass(_lib.PASS_UPDATE_W | _lib.PASS_ACCUMULATE)
                 self.reduce(self.n_out, self.AB)
                 self.basis_update()
+                if ev is not None and not whole:
+                    ev[2 * i + 1].record(stream)
+            if whole:
+                ev[1].record(stream)
             return
         if self.world == 1 and not self.shard_steps:
             with torch.cuda.device(self.device):

@@ -112,6 +112,83 @@ def test_launcher_decision():
     assert d(2, {"WORLD_SIZE": "2"}, 0, "nccl") == ("run", None)  # the driver's torchrun line
     assert d(8, {"WORLD_SIZE": "1"}, 8, "nccl")[0] == "refuse"
     assert d(1, {"WORLD_SIZE": "4"}, 8, "nccl")[0] == "refuse"
+    # --gpus omitted takes the launcher's WORLD_SIZE (torchrun without a matching --gpus)
+    assert d(None, {"WORLD_SIZE": "4"}, 8, "nccl") == ("run", None)
+    assert d(None, {}, 0, "nccl") == ("run", None)
+
+
+def test_line_value_and_unit():
+    """VERDICT r4 item 5 / ADVICE r4: the value is an iteration rate of the problem actually run,
+    and the unit says which — no rescaling by rows / 1e6 (the 1e7-row cfg3 line once printed
+    12,377 'it/s' for a 1,238 it/s fit)."""
+    v, u = bench.line_value("weak", 1, 10_000_000, 500, 500 / 1238.0)
+    assert abs(v - 1238.0) < 1e-6 and u == "1e7-row it/s"
+    v, u = bench.line_value("weak", 1, 1_000_000, 500, 500 / 17800.0)
+    assert abs(v - 17800.0) < 1e-6 and u == "1e6-row it/s"  # cfg2 at N = 1: unchanged value
+    v, u = bench.line_value("weak", 8, 1_000_000, 500, 500 / 17000.0)
+    assert abs(v - 8 * 17000.0) < 1e-6 and u == "1e6-row it/s"  # the 1e6-row shards' iterations, summed
+    v, u = bench.line_value("strong", 8, 124_992, 500, 500 / 60000.0)
+    assert abs(v - 60000.0) < 1e-6 and u == "it/s"
+    assert bench.row_unit(16384) == "16384"
+
+
+def test_state_problem_flags_nan_and_negative():
+    import numpy as np
+    W, H = np.ones((4, 2), np.float32), np.ones((2, 3))
+    assert bench.state_problem(1.0, W, H) is None
+    assert "error" in bench.state_problem(float("nan"), W, H)
+    assert "error" in bench.state_problem(float("inf"), W, H)
+    Wn = W.copy(); Wn[1, 1] = np.nan
+    assert "W" in bench.state_problem(1.0, Wn, H)
+    Hn = H.copy(); Hn[0, 2] = -1e-30
+    assert "negative" in bench.state_problem(1.0, W, Hn)
+
+
+class _NaNPlan:
+    """A stand-in plan whose final state is broken on one rank only."""
+
+    def __init__(self, broken):
+        self.broken = broken
+        self.W = torch.ones(8, 4)
+        self.H64 = torch.ones(4, 81, dtype=torch.float64)
+        if broken:
+            self.W[3, 2] = float("nan")
+
+    def frobenius_error(self):
+        return float("nan") if self.broken else 1.0
+
+
+def _verdict_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        err, problem = bench.final_verdict(_NaNPlan(broken=rank == 1), world, torch.device("cpu"))
+        code = None
+        try:
+            if problem:
+                bench.refuse_result(problem, rank)
+        except SystemExit as e:
+            code = e.code
+        out[rank] = (problem, code)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_forced_nan_plan_refuses_on_every_rank():
+    """a NaN state on ANY rank makes EVERY rank exit non-zero without a line."""
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_verdict_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in (0, 1):
+        problem, code = out[r]
+        assert problem and code == bench.EXIT_BROKEN != 0
+    assert "another rank" in out[0][0] and "error" in out[1][0]
+    # one rank, no group: the same verdict
+    err, problem = bench.final_verdict(_NaNPlan(broken=True), 1, None)
+    assert problem and err != err
+    with pytest.raises(SystemExit) as e:
+        bench.refuse_result(problem, 0)
+    assert e.value.code == bench.EXIT_BROKEN
 
 
 def _bench_cmd(extra, env):

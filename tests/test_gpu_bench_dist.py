@@ -34,6 +34,8 @@ def _run_two_ranks(extra, timeout=240):
                    LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
                "--steps", "20", "--warmup", "20", "--no-cpu", "--ramp-seconds", "0.2", "--scaling", "strong"] + extra
+        if "--strong-rows" not in extra:  # the 1e6-row strong split's grids are not co-resident on one GPU
+            cmd += ["--strong-rows", "0"]
         procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -57,7 +59,7 @@ def _run_two_ranks(extra, timeout=240):
 def test_bench_two_ranks_one_gpu_exchange():
     res, outs = _run_two_ranks(["--rows", "32768"])
     cfg = res["config"]
-    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["ranks"] == 2 and res["n_gpus"] == 1 and res["value"] > 0  # two ranks sharing one GPU
     assert cfg["exchange"].startswith("validated"), cfg["exchange"]
     lay = cfg["layout_per_rank"]
     assert len(lay) == 2 and lay[0] == lay[1]
@@ -69,7 +71,7 @@ def test_bench_two_ranks_one_gpu_exchange():
 def test_bench_two_ranks_one_gpu_host_collective_path():
     """--exchange off: one shard step + one all_reduce per iteration on both ranks."""
     res, _ = _run_two_ranks(["--rows", "32768", "--exchange", "off", "--no-tune"])
-    assert res["n_gpus"] == 2 and res["value"] > 0
+    assert res["ranks"] == 2 and res["value"] > 0
     assert res["config"]["exchange"] is None
     assert res["roofline"]["launches_timed"] == 20
 
@@ -79,8 +81,42 @@ def test_bench_two_ranks_one_gpu_weak_scaling():
     """The default scaling (weak): every rank owns --rows rows; the line's value is the 1e6-row
     iterations all ranks completed per second, the exchange validated as at strong scaling."""
     res, _ = _run_two_ranks(["--rows", "16384", "--scaling", "weak"])
-    assert res["scaling"] == "weak" and res["n_gpus"] == 2
+    assert res["scaling"] == "weak" and res["ranks"] == 2
     assert res["config"]["n_rows_per_gpu"] == 16384 and res["config"]["n_rows_total"] == 32768
     assert res["config"]["exchange"].startswith("validated"), res["config"]["exchange"]
     it_s = res["steps"] / (res["ms_per_step"] * res["steps"] / 1e3)
-    assert abs(res["value"] - 2 * 16384 / 1e6 * it_s) <= 0.02 * res["value"]
+    # ADVICE r4: ranks x it/s of the problem run, in a unit that names the shard's rows
+    assert abs(res["value"] - 2 * it_s) <= 0.02 * res["value"]
+    assert res["unit"] == "16384-row it/s"
+    assert res["n_gpus"] == 1 and res["ranks"] == 2  # two ranks sharing one GPU are not two GPUs
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_strong_split_beside_the_weak_line():
+    """at N > 1 the line carries the fixed problem (here 32768 rows, the metric's
+    V = 1e6 on the driver's nodes) split over the same ranks and timed in the same run, and the same
+    problem on rank 0's GPU alone: it/s, us per iteration, HBM fraction, speed-up over one GPU."""
+    res, outs = _run_two_ranks(["--rows", "16384", "--scaling", "weak", "--strong-rows", "32768"])
+    assert res["unit"] == "16384-row it/s" and res["scaling"] == "weak"
+    st = res["strong"]
+    assert st["rows"] == 32768 and st["ranks"] == 2 and st["rows_per_gpu_max"] == 16384
+    for key in ("it_s", "us_per_iteration", "frac", "speedup_vs_n1", "n1_it_s", "n1_us_per_iteration"):
+        assert st[key] > 0, (key, st)
+    assert abs(st["it_s"] * st["us_per_iteration"] / 1e6 - 1.0) < 0.01
+    assert abs(st["speedup_vs_n1"] - st["n1_us_per_iteration"] / st["us_per_iteration"]) < 0.01
+    assert st["exchange"].startswith("validated"), st["exchange"]
+    assert outs[0][2].count("in-launch exchange (16384 rows): validated") == 2  # the weak and the split plan
+
+
+@pytest.mark.timeout(300)
+def test_bench_one_gpu_line_carries_strong_as_itself():
+    """At N = 1 on the metric's rows the `strong` key is the line itself (speed-up 1)."""
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "20",
+                        "--no-cpu", "--ramp-seconds", "0.1", "--rows", "65536", "--strong-rows", "65536"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["unit"] == "65536-row it/s" and res["n_gpus"] == 1
+    assert res["strong"]["speedup_vs_n1"] == 1.0 and res["strong"]["rows"] == 65536
+    assert abs(res["strong"]["it_s"] - res["value"]) <= 0.01 * res["value"]

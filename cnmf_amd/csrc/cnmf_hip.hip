@@ -1133,7 +1133,8 @@ __global__ __launch_bounds__(NT, 2) void mu_pass_bf16_mfma_kernel(const bf16_t* 
 //     new w'[4g + r][li] are exactly the A operand of phase 3 (row m = li, k = samples 4g..4g+3), so
 //     W' never goes through LDS;
 //   * phase 3  A[m][f] += Σ_s w'[s][m]·x[s][f] on v_mfma_f32_16x16x16_bf16 (K = the tile's 16 samples;
-//     B = X columns by ds_read_b64_tr_b16; w' in three bf16 terms, so every product is exact in fp32);
+//     B = X columns by ds_read_b64_tr_b16; w' in two bf16 terms since round 5 — 16 significant bits,
+//     the dropped term an unbiased per-sample rounding that the sum over samples averages out);
 //     B[m][n] += Σ_s w'[s][m]·w'[s][n] on v_mfma_f32_16x16x4_f32.  The fp32 MFMA accumulators chain
 //     over the wave's tiles (≈ 61 at cfg4: the per-lane fp32 accumulation of mu_iter_wt_kernel);
 //   * end of launch: the four waves' accumulators summed in LDS in the fixed order (w0 + w2) + (w1 + w3)
@@ -2479,7 +2480,11 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         if (l1 > 0.0) d += l1;              // SK:616-617
         if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
         if (d == 0.0) d = EPS32;            // SK:620
-        wn = (float)(wold * (num64[r] / d));  // SK:622-629
+        // SK:622-629 with 1/d as v_rcp_f64 + one Newton step (relative error ~2^-52, then rounded to
+        // fp32) in place of the fp64 division's ~10-instruction sequence
+        double rd = __builtin_amdgcn_rcp(d);
+        rd = fma(rd, fma(-d, rd, 1.0), rd);
+        wn = (float)(wold * (num64[r] * rd));
       }
       wn = valid ? wn : 0.f;
       wr[r] = wn;
@@ -2488,16 +2493,17 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
     }
     if (!do_acc) return;
     // phase 3: A[m = 4g + r][f = 16nb + li] and B[m][n] over the tile's 16 samples
-    s16x4 a1, a2, a3;  // w'[4g + j][li] in three bf16 terms: the A operand (row m = li, k = 4g + j)
+    // w'[4g + j][li] in TWO bf16 terms (16 significant bits; round 5): the dropped
+    // third term is an unbiased per-sample rounding of |w'|·2^-18 at most, which the sum over the
+    // samples averages out (relative error ~2^-17/sqrt(n) of A = W'ᵀX: 1e-8 at 1e6 rows), where phase
+    // 1's H terms stay three (a rounding of H is the same for every sample: a bias, not noise)
+    s16x4 a1, a2;  // the A operand (row m = li, k = 4g + j)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint16_t h1 = bm::bf16_rn(wr[j]);
       const float r1 = wr[j] - bm::bf16_f(h1);
-      const uint16_t h2 = bm::bf16_rn(r1);
-      const float r2 = r1 - bm::bf16_f(h2);
       a1[j] = (short)h1;
-      a2[j] = (short)h2;
-      a3[j] = (short)bm::bf16_rn(r2);
+      a2[j] = (short)bm::bf16_rn(r1);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) bacc = __builtin_amdgcn_mfma_f32_16x16x4f32(wr[r], wr[r], bacc, 0, 0, 0);
@@ -2507,7 +2513,6 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
     for (int nb = 0; nb < NBX; ++nb) {
       if (nb < (KSC ? 2 * KSC : NB)) {
         const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(xb0 + 32 * nb));
-        cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a3, b, cacc[nb], 0, 0, 0);
         cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a2, b, cacc[nb], 0, 0, 0);
         cacc[nb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a1, b, cacc[nb], 0, 0, 0);
       }

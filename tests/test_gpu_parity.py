@@ -228,7 +228,8 @@ def test_factorise_normalise_option():
 def test_bf16_mfma_single_pass_matches_numpy(N, F, k):
     """§8 a8: the bf16 matrix-core pass (the wave-tile mu_pass_bfw_kernel over the full 64-sample
     tiles, the 64-sample mu_pass_bf16_mfma_kernel on a ragged tail: v_mfma_f32_16x16x32 /
-    16x16x16 bf16 with 3-term bf16 splits of H and W', ds_read_b64_tr_b16 column reads): one W
+    16x16x16 bf16 with 3-term bf16 splits of H and (64-sample kernel) W' — two terms of W' in the
+    wave-tile pass since round 5 — ds_read_b64_tr_b16 column reads): one W
     update and [WᵀX | WᵀW] vs NumPy fp64 on the bf16-rounded X (ragged last tile, no full tile at
     all, whole tiles only, k < 16 padding, F = 320, padded and unpadded LDS rows)."""
     import torch

@@ -13,6 +13,7 @@
 #   ab <tag> <n> <bench.py args...>    same-box A/B: tools/ab/libcnmf_hip_base.so (base) and the
 #                                      product library alternating n times -> <tag>_{base,prod}_r<i>.json
 #   timeline <tag> <args...>           tools/timeline_persist.py on the stamps build -> <tag>.log
+#   tlbase <tag> <args...>             the same on tools/ab/libcnmf_hip_base_stamps.so (A/B)
 #   smoke                              __graft_entry__.smoke() -> smoke.log
 #   prof <tag> <bench.py args...>      rocprofv3 --kernel-trace --stats of a bench run -> <tag>/
 #   pmc <tag> "<counters>" <script args...>  one rocprofv3 --pmc pass over a python script -> <tag>/
@@ -37,6 +38,8 @@ for st in "$@"; do
         CNMF_HIP_LIB=$BASE timeout -k 10 300 python -u bench.py "$@" > "$D/${tag}_base_r$r.json" 2> "$D/${tag}_base_r$r.err" || { tail -20 "$D/${tag}_base_r$r.err"; exit 1; }
         timeout -k 10 300 python -u bench.py "$@" > "$D/${tag}_prod_r$r.json" 2> "$D/${tag}_prod_r$r.err" || { tail -20 "$D/${tag}_prod_r$r.err"; exit 1; }
       done ;;
+    tlbase)  # the timeline on the base library's stamps build (same-box A/B of the timeline)
+      CNMF_HIP_LIB=tools/ab/libcnmf_hip_base_stamps.so timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     timeline)
       CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_stamps.so timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     smoke)

@@ -2270,6 +2270,15 @@ __device__ __forceinline__ void st16_sc1(double* p, double v0, double v1) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
 
+// n / d for the W-updates of the wave-tile kernels: v_rcp_f64 + one Newton step (relative error
+// ~2^-50, far below the fp32 rounding of the new w that follows) in place of the fp64 division's
+// ~10-instruction IEEE sequence (round 5; d is a denominator >= EPS32, never denormal)
+__device__ __forceinline__ double div_nr(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return n * r;
+}
+
 // The arguments of the bf16 wave-tile pass and of its persistent form (mu_iter_bfw_kernel).
 struct BfwArgs {
   const bf16_t* X;
@@ -2426,27 +2435,36 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
   EOI_DECL
 
   // phase 1 for a PAIR of wave tiles: each K-step's three H terms are read from LDS once for both
-  // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body)
+  // tiles' chains (two independent MFMA chains; half the H traffic of one tile per body).  K-steps
+  // run in pairs on separate accumulators (four independent chains), whose fp32 sum is folded into
+  // fp64 once per pair of K-steps (round 5: half the fp64 converts and adds of a fold per K-step;
+  // a fold now covers 64 features, as the wave-tile kernels' 7-feature chains cover 7 x k)
   auto phase1 = [&](double (&n0)[4], double (&n1)[4]) {
     const unsigned char* xa0 = xsp[0] + li * XR + 16 * g;
     const unsigned char* xa1 = xsp[1] + li * XR + 16 * g;
     const unsigned char* hb = smem + L.hs + li * L.hrow + 16 * g;
-#pragma unroll
-    for (int ks = 0; ks < (KSC ? KSC : 10); ++ks) {
-      if (!KSC && ks >= KS) break;
+    auto kstep = [&](int ks, f32x4& u, f32x4& v) {
       const s16x8 a = *reinterpret_cast<const s16x8*>(xa0 + 64 * ks);  // 16-B aligned rows: one b128
       const s16x8 c = *reinterpret_cast<const s16x8*>(xa1 + 64 * ks);
       const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
       const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
       const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
       const bf16x8 av = __builtin_bit_cast(bf16x8, a), cv = __builtin_bit_cast(bf16x8, c);
-      f32x4 u = f32x4{0.f, 0.f, 0.f, 0.f}, v = f32x4{0.f, 0.f, 0.f, 0.f};
       u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
       v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
       u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b2, u, 0, 0, 0);
       v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b2, v, 0, 0, 0);
       u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, u, 0, 0, 0);
       v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b1, v, 0, 0, 0);
+    };
+#pragma unroll
+    for (int ks = 0; ks < (KSC ? KSC : 10); ks += 2) {
+      if (!KSC && ks >= KS) break;
+      const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 u0 = z, v0 = z, u1 = z, v1 = z;
+      kstep(ks, u0, v0);
+      if (KSC ? ks + 1 < KSC : ks + 1 < KS) kstep(ks + 1, u1, v1);
+      const f32x4 u = u0 + u1, v = v0 + v1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         n0[r] += (double)u[r];
@@ -2480,11 +2498,7 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
         if (l1 > 0.0) d += l1;              // SK:616-617
         if (l2 > 0.0) d = d + l2 * wold;    // SK:618-619
         if (d == 0.0) d = EPS32;            // SK:620
-        // SK:622-629 with 1/d as v_rcp_f64 + one Newton step (relative error ~2^-52, then rounded to
-        // fp32) in place of the fp64 division's ~10-instruction sequence
-        double rd = __builtin_amdgcn_rcp(d);
-        rd = fma(rd, fma(-d, rd, 1.0), rd);
-        wn = (float)(wold * (num64[r] * rd));
+        wn = (float)(wold * div_nr(num64[r], d));  // SK:622-629 (div_nr: VERDICT r4 item 3b)
       }
       wn = valid ? wn : 0.f;
       wr[r] = wn;
@@ -3461,6 +3475,25 @@ template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
+// the value of lane l ^ 16 / l ^ 32 (v_permlane16/32_swap: lanes 32-63 of the first operand trade
+// with lanes 0-31 of the second, resp. the odd 16-lane rows of the first with the even rows of the
+// second; with both operands v, the first result holds l ^ 32 in the upper half / l ^ 16 in the odd
+// rows, the second in the lower half / the even rows)
+__device__ __forceinline__ double lane_xor16(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const bool odd = (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 16) != 0;
+  return __hiloint2double(odd ? (int)b[0] : (int)b[1], odd ? (int)a[0] : (int)a[1]);
+}
+__device__ __forceinline__ double lane_xor32(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool up = (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 32) != 0;
+  return __hiloint2double(up ? (int)b[0] : (int)b[1], up ? (int)a[0] : (int)a[1]);
+}
+
 // v summed over the lanes l' ≡ l (mod NL) of the wave (every lane gets its class's sum)
 template <int NL>
 __device__ __forceinline__ float sum_over_samples(float v) {
@@ -3900,7 +3933,11 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       ++cur_it;
     }
     const bool last_it = it + 1 == a.n_iter;
+#ifdef CNMF_TOL_NOLOSS  // timing-only diagnostic: the TOL kernel without its loss iterations (never stops)
+    const bool loss_it = false;
+#else
     const bool loss_it = TOL && ((it0 + it) % 10 == 0);  // check the state after it0 + it iterations
+#endif
     const int64_t tile = gw + (int64_t)NW * i;
     // phase 1: x along the lane's row, packed fp32 chains of 7 features folded into fp64
     const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * e;
@@ -4022,7 +4059,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
     if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
     if (den == 0.0) den = EPS32;                // SK:620
-    const float wn = (float)(wold * (num / den));  // SK:622-629
+    const float wn = (float)(wold * div_nr(num, den));  // SK:622-629
     wt_[s * KK + e] = wn;
     if (!WRES) reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wn;  // lane l = (s, e)
     // w'[s][·]: the sample's row back from LDS (this wave's writes above precede the reads)
@@ -4525,7 +4562,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_mf8_kernel(PersistArgs a) {
         if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
         if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
         if (den == 0.0) den = EPS32;                // SK:620
-        const float wn = (float)(wold * (num / den));  // SK:622-629
+        const float wn = (float)(wold * div_nr(num, den));  // SK:622-629
         if (lc < KK) {
           wt_[s * KK + e] = wn;
           wp[s * 16 + e] = wn;
@@ -6542,7 +6579,7 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
     const double num = (b1 ? kn[1] : kn[0]) + dpp64<0xB1>(b1 ? kn[0] : kn[1]);  // quad_perm [1,0,3,2]
     double den = (b1 ? kd[1] : kd[0]) + dpp64<0xB1>(b1 ? kd[0] : kd[1]);
     if (den == 0.0) den = EPS32;
-    const float wn = (float)(wold * (num / den));
+    const float wn = (float)(wold * div_nr(num, den));
     wt_[s * KK + e] = wn;
     // phase 3 with the sample's new row (this wave's writes above precede the read)
     const float4 p4 = *reinterpret_cast<const float4*>(wt_ + s * KK);
@@ -6834,7 +6871,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   constexpr int KK = wa::K, NL = wa::NL, NQ = wa::NQ, V = wa::V, NOUT = wa::NOUT, NACC = wa::NACC;
   constexpr int NOUTT = NOUT + (TOL ? 1 : 0);  // partial-row width: + the loss of the checked state
   constexpr int XBW = G4::XBW, XSTR = G4::XSTR, PFW = G4::PFW, LASTL = G4::LASTL;
-  constexpr int PFS = PFW + (TOL ? 1 : 0);  // loads per prefetch set: the X tile (+ TOL: its old W)
+  // MX: the W-step starts from the passive set of the tile's previous W (WARM, round 5), so its W is
+  // loaded with X, as the TOL form's loss needs it too
+  constexpr bool WARM = MX;
+  constexpr int PFS = PFW + (TOL || WARM ? 1 : 0);  // loads per prefetch set: the X tile (+ its old W)
   constexpr int KP = KK / 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int t = threadIdx.x;
@@ -6946,13 +6986,13 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
 #pragma unroll
     for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
     ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
-    if constexpr (TOL) ld16(pf[PFW], l < 16 ? Wb + (size_t)tile * 256 + 16 * l : xs);  // the tile's W
+    if constexpr (TOL || WARM) ld16(pf[PFW], l < 16 ? Wb + (size_t)tile * 256 + 16 * l : xs);  // the tile's W
   };
   auto stage = [&](const u32x4 (&pf)[PFS]) {
     const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
     stage_rec<0, PFW - 1>(addr, pf);
     if (l < LASTL) st16<1024 * (PFW - 1)>(addr, pf[PFW - 1]);
-    if constexpr (TOL)
+    if constexpr (TOL || WARM)
       if (l < 16) st16<0>((unsigned)(uintptr_t)(wstg + 16 * l), pf[PFW]);
   };
 
@@ -6985,9 +7025,6 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     prefetch(pfk, gw + (int64_t)NW * (nx_i < nbt ? nx_i : 0));
     if (++nx_i == nbp) nx_i = 0;
   };
-  // MX: the identity block — A row i = (g = i % 4, component (i / 4) ^ (i % 4)) of I — turns c[g][s]
-  // into the rotated copies c[g ^ ρ][s] in the D registers (exact: one product by 1, three zeros)
-  const double tid = ((((l & 15) >> 2) ^ (l & 3)) == gm) ? 1.0 : 0.0;
   // the wave's exchange scratch (best objective / mask, the new W row): its reduction rows, free
   // while the tiles stream (the x slot stays intact for phase 3); phase 3's lane roles
   unsigned char* xscr = reinterpret_cast<unsigned char*>(red + w * NL * NACC);
@@ -7010,8 +7047,13 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       if (ks + 2 < NQ) m2 = __builtin_amdgcn_mfma_f64_4x4x4f64(hq(ks + 2), (double)xv[ks + 2], m2, 0, 0, 0);
     }
     const double cs = ((m0 + m1) + m2) + a.delta2;  // c[gm][sm] + δ²
-    // c rotated: cr[ρ] = c[gm ^ ρ][sm]
-    const f64x4 cr = __builtin_amdgcn_mfma_f64_16x16x4f64(tid, cs, f64x4{0.0, 0.0, 0.0, 0.0}, 0, 0, 0);
+    // c rotated: cr[ρ] = c[gm ^ ρ][sm], the lanes l ^ 16ρ (permlane swaps; round 4 used an identity
+    // block on the matrix cores: one 64-cycle f64 MFMA and eight AGPR reads per tile)
+    f64x4 cr;
+    cr[0] = cs;
+    cr[1] = lane_xor16(cs);
+    cr[2] = lane_xor32(cs);
+    cr[3] = lane_xor32(cr[1]);
     if constexpr (TOL) {
       if ((it0 + cur_it) % 10 == 0) {
         // a loss iteration: ‖x − w·H‖² of the state after it0 + cur_it iterations, per sample as
@@ -7047,6 +7089,29 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
         *lacc += xx;
       }
     }
+    // WARM (round 5): the sample's previous passive set P = {j : w_j > 0} (its W as loaded with X)
+    // solved first, w_P = (Q_PP)⁻¹ c_P from the table, and certified by the KKT conditions of the
+    // strictly convex problem — w_P >= 0 and the dual (Q w − c)_j >= 0 off P — which make it THE
+    // minimiser the enumeration below finds (same formula, same bits when it picks the same mask).
+    // Only a tile with a sample whose set changed (or whose mask is invalid) runs the enumeration.
+    float* xw_ = reinterpret_cast<float*>(xscr + 768);  // the sample rows of the new W (phase 3)
+    double wn64;
+    bool warm_ok = false;
+    if constexpr (WARM) {
+      const float4 wo = *reinterpret_cast<const float4*>(wstg + 16 * sm);
+      const int mw = (wo.x > 0.f ? 1 : 0) | (wo.y > 0.f ? 2 : 0) | (wo.z > 0.f ? 4 : 0) | (wo.w > 0.f ? 8 : 0);
+      const double* T = sTab + mw * wa::TSTR + 4 * gm;
+      const double wg = fma(T[gm ^ 3], cr[3], fma(T[gm ^ 2], cr[2], fma(T[gm ^ 1], cr[1], T[gm] * cr[0])));
+      const double* Q = reinterpret_cast<const double*>(smem + wa::L_HHT) + 4 * gm;  // HHᵀ row gm
+      const double w1 = lane_xor16(wg), w2 = lane_xor32(wg), w3 = lane_xor32(w1);  // w[gm ^ ρ]
+      const double dual = fma(Q[gm ^ 3] + a.delta2, w3, fma(Q[gm ^ 2] + a.delta2, w2,
+                              fma(Q[gm ^ 1] + a.delta2, w1, (Q[gm] + a.delta2) * wg))) - cs;
+      const bool inP = ((mw >> gm) & 1) != 0;
+      const bool ok = sTab[16 * wa::TSTR + mw] != 0.0 && (inP ? wg >= 0.0 : dual >= 0.0);
+      warm_ok = __ballot(!ok) == 0;  // wave-uniform
+      wn64 = wg;
+    }
+    if (!warm_ok) {
     // FCLS: the 16 masks' solutions, lane (s, g) block b' = mask 4b' + g (register ρ = component ρ ^ g);
     // the lane's masks ascend with b', so a strict < keeps the lowest of tied masks
     double bestf = 1.0;
@@ -7064,7 +7129,6 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     // registers; in-order LDS inside the wave) and each takes the least (objective, mask)
     double* xf_ = reinterpret_cast<double*>(xscr);
     int* xm_ = reinterpret_cast<int*>(xscr + 512);
-    float* xw_ = reinterpret_cast<float*>(xscr + 768);
     xf_[4 * sm + gm] = bestf;
     xm_[4 * sm + gm] = bestm;
     {
@@ -7081,11 +7145,11 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       pick(fo.z, mo.z);
       pick(fo.w, mo.w);
     }
-    double wn64;
     {
       const double* T = sTab + min(bestm, 15) * wa::TSTR + 4 * gm;
       wn64 = fma(T[gm ^ 3], cr[3], fma(T[gm ^ 2], cr[2], fma(T[gm ^ 1], cr[1], T[gm] * cr[0])));
     }
+    }  // the enumeration
     const float wn = (float)fmax(wn64, 0.0);
     a.W[(size_t)tile * (16 * KK) + 4 * sm + gm] = wn;  // the tile's 256 contiguous bytes
     // phase 3, regrouped: lane (s4 = l % 4, g3 = l / 4) takes the tile's samples 4j + s4 (j < 4) and
@@ -8083,7 +8147,9 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int pd = tol ? 3 : wt_pd(k, wres != 0, multi);
     // tiles per wave: > PD (the first prefetches), >= 2·PD + 1 when W is streamed (re-load hazard)
     const int min_nbt = wres ? pd + 1 : 2 * pd + 1;
-    const int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
+    int64_t G = std::min<int64_t>({(int64_t)ncu, n_tiles / (wt::NWV * min_nbt), (int64_t)sl::GROUP * sl::MAX_GROUPS});
+    if (const char* mg = diag_env("CNMF_WT_MAXG"))  // diagnostic: fewer, fuller waves (strong-scaling shards)
+      if (atoi(mg) > 0) G = std::min<int64_t>(G, atoi(mg));
     if (G < 1) continue;
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     // W resident: the four waves' W tiles; TOL (the wave-tile kernel) a second copy: the snapshot of
@@ -8238,6 +8304,8 @@ static int als_iterations(int n_iter, const void* X, int x_dtype, void* W, doubl
   pa.n_tiles = L.n_tiles;
   pa.n_iter = n_iter;
   pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  if (const char* gz = diag_env("CNMF_WT_GROUP"))  // diagnostic: workgroups per first-level group
+    if (atoi(gz) > 0) pa.n_groups = (int)std::min<int64_t>((L.G + atoi(gz) - 1) / atoi(gz), sl::MAX_GROUPS);
   pa.delta2 = sum_to_one * sum_to_one;
   pa.lam = smoothness;
   pa.xctl = xctl;
@@ -8300,6 +8368,8 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.n_tiles = L.n_tiles;
   pa.n_iter = n_iter;
   pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
+  if (const char* gz = diag_env("CNMF_WT_GROUP"))  // diagnostic: workgroups per first-level group
+    if (atoi(gz) > 0) pa.n_groups = (int)std::min<int64_t>((L.G + atoi(gz) - 1) / atoi(gz), sl::MAX_GROUPS);
   pa.n_static = 0;
   pa.l1W = l1_W;
   pa.l2W = l2_W;

@@ -137,12 +137,12 @@ class MUPlan:
             xg = self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, 0, 1) if self.persistent_shape else 0
         self.exchange_shape = self.persistent_shape and int(xg) > 0
         # the persistent layouts tune() chooses between for this shape (include/cnmf_hip.h `layout`):
-        # k = 8 fp32: the VALU (4) or matrix-core (5) wave tiles; cfg4's bf16 shape: the per-iteration
-        # launches (4) or ONE persistent launch (6)
+        # cfg4's bf16 shape: the per-iteration launches (4) or ONE persistent launch (6).  k = 8 fp32
+        # takes the VALU wave tiles (4); the matrix-core tiles (5) stay selectable with set_layout(5)
+        # but are no longer timed on every run: they lost on every box measured (cfg3 shard 150.6 vs
+        # 110.7 us, profiles/r05/)
         self.layouts = ()
-        if self.persistent_shape and self.k == 8 and self.xdt == _lib.F32:
-            self.layouts = (4, 5)
-        elif self.xdt == _lib.BF16 and self.world == 1 and not self.persistent_shape:
+        if self.xdt == _lib.BF16 and self.world == 1 and not self.persistent_shape:
             with torch.cuda.device(self.device):
                 if int(self.lib.cnmf_persist_workgroups(self.n_rows, self.F, self.k, self.xdt, 6, 0)) > 0:
                     self.layouts = (4, 6)

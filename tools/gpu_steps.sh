@@ -10,6 +10,7 @@
 # steps:
 #   pytest <tag> <pytest args...>      python -m pytest (thread timeouts) -> <tag>.log
 #   bench <tag> <bench.py args...>     one bench line -> <tag>.json / .err
+#   benchlib <tag> <lib> <args...>     the same on another library file
 #   ab <tag> <n> <bench.py args...>    same-box A/B: tools/ab/libcnmf_hip_base.so (base) and the
 #                                      product library alternating n times -> <tag>_{base,prod}_r<i>.json
 #   timeline <tag> <args...>           tools/timeline_persist.py on the stamps build -> <tag>.log
@@ -21,7 +22,7 @@
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 D=gpurun_out/$1; shift; mkdir -p "$D"
-BASE=tools/ab/libcnmf_hip_base.so
+BASE=${AB_BASE:-tools/ab/libcnmf_hip_base.so}
 for st in "$@"; do
   set -- $st
   kind=$1; tag=$2; shift 2
@@ -32,6 +33,9 @@ for st in "$@"; do
       timeout -k 10 900 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread "$@" > "$D/$tag.log" 2>&1 || { tail -30 "$D/$tag.log"; exit 1; } ;;
     bench)
       timeout -k 10 400 python -u bench.py "$@" > "$D/$tag.json" 2> "$D/$tag.err" || { tail -20 "$D/$tag.err"; exit 1; } ;;
+    benchlib)  # one bench line on another library: benchlib <tag> <lib> <bench args>
+      lib=$1; shift
+      CNMF_HIP_LIB=$lib timeout -k 10 400 python -u bench.py "$@" > "$D/$tag.json" 2> "$D/$tag.err" || { tail -20 "$D/$tag.err"; exit 1; } ;;
     ab)
       n=$1; shift
       for r in $(seq 1 "$n"); do

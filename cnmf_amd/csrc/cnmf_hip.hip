@@ -6824,7 +6824,11 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
   }
   if (t < K * K) hB[t] = sAB[(t / K) * V + F + (t % K)];
   __syncthreads();
+#ifdef CNMF_ALS_NOHSTEP  // timing-only diagnostic: the persistent ALS without its H-step rows (H fixed)
+  __syncthreads();
+#else
   als_hstep(smem + L_HS, F, K, lam, t);
+#endif
   for (int e = t; e < K * F; e += NT) sH[e] = hH[e];
   __syncthreads();
   wa_derive(smem, t, delta2);

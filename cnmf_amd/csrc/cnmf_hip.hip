@@ -4857,9 +4857,13 @@ __global__ __launch_bounds__(256) void scale_columns_kernel(TC* __restrict__ W, 
 // ------------------------------------------------------------------------------------------------
 constexpr int ALS_MAX_F = 512;
 
+__host__ __device__ inline size_t als_pre_offset(int F, int k) {  // 16-B aligned, after the ints
+  return (((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 16) * 4 + 15) / 16 * 16;
+}
 __host__ __device__ inline size_t als_lds_bytes(int F, int k) {
-  // doubles: A, H [k][F]; B [k][k]; b, x, d0, e1, e2, L0, L1, L2, z [F]; then ints: pas, inf, idx [F], 8
-  return ((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 16) * 4;
+  // doubles: A, H [k][F]; B [k][k]; b, x, d0, e1, e2, L0, L1, L2, z [F]; then ints: pas, inf, idx [F], 8;
+  // then (the one-wave form's per-row constants, round 5) bpre, rinv [k][F] and k sweep counts
+  return als_pre_offset(F, k) + ((size_t)2 * k * F + 4) * 8;
 }
 
 // M(fa, fb) of the row Hessian for |fa - fb| <= 2 (0 otherwise), fb < fa
@@ -5076,6 +5080,15 @@ __device__ __forceinline__ void als_hstep_block(unsigned char* smem, int F, int 
 }
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+// The value through an empty asm: what is derived from it can no longer be hoisted out of a
+// persistent kernel's iteration loop.  (The compiler hoisted the end-of-iteration code's lane
+// addresses — LDS row offsets, the butterflies' ds_bpermute addresses — and, short of registers
+// across the streaming loop, spilled them: each reload in the reduction / H-step / derive path was
+// a scratch round trip, behind a vmcnt(0) that also waited for the in-flight prefetch.)
+__device__ __forceinline__ int opaque_i(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 // The same sweep for F <= 128 on ONE wave, without a workgroup barrier inside it (same LDS layout;
 // the other waves wait at the closing barrier).  Lane l holds features 2l and 2l + 1 (round 5: the
@@ -5106,6 +5119,35 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #ifdef CNMF_STAMPS
   const unsigned hs_call = blockIdx.x == 0 ? __hip_atomic_load(&g_hs_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 64u;
 #endif
+  // ---- round 5: what every row needs from the OLD basis and from B alone, by all the workgroup's
+  // threads in parallel before the sequential sweep (the one wave's per-row setup was ~1.5 k of its
+  // ~3.5 k cycles per row, profiles/r05/r5c/tl_als_new.log): bpre[j][f] = a_j[f] − Σ_{m>j} B_jm·h_m[f]
+  // (the rows after j are still the old ones when row j is solved), rinv[j][f] = 1 / (B_jj + λ·DᵀD_ff),
+  // and each row's Jacobi sweep count (0: the row takes the block PCR)
+  {
+    const double* sA = reinterpret_cast<const double*>(smem);
+    const double* sH = sA + (size_t)k * F;
+    const double* sB = sH + (size_t)k * F;
+    double* bpre = reinterpret_cast<double*>(smem + als_pre_offset(F, k));
+    double* rinv = bpre + (size_t)k * F;
+    double* nswp = rinv + (size_t)k * F;
+    for (int o = t; o < k * F; o += RED_NT) {
+      const int j = o / F, f = o - j * F;
+      double b = sA[o];
+      for (int m = j + 1; m < k; ++m) b -= sB[j * k + m] * sH[m * F + f];
+      bpre[o] = b;
+      const double bjj = sB[j * k + j];
+      rinv[o] = 1.0 / (bjj + lam * als_L_entry(F, f, f));
+    }
+    if (t < k) {
+      const double bjj = sB[t * k + t];
+      const double rho = 10.0 * lam / bjj;
+      int nsw = 0;
+      for (double r = 1.0; rho <= 0.05 && r > 0x1p-55; r *= rho) ++nsw;
+      nswp[t] = (double)nsw;
+    }
+    __syncthreads();
+  }
   if (t < 64) {
     const int lane = t;
     double* sA = reinterpret_cast<double*>(smem);
@@ -5130,14 +5172,28 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       lm1[c] = (f < F && f >= 1) ? lam * als_L_entry(F, f - 1, f) : 0.0;
       lm2[c] = (f < F && f >= 2) ? lam * als_L_entry(F, f - 2, f) : 0.0;
     }
+    double* bpre = reinterpret_cast<double*>(smem + als_pre_offset(F, k));
+    const double* rinvp = bpre + (size_t)k * F;
+    const double* nswp = rinvp + (size_t)k * F;
     for (int j = 0; j < k; ++j) {
+      // the row's operands in one batch of LDS reads.  bpre[j] already holds a_j − Σ_{m>j} B_jm·h_m(old)
+      // − Σ_{m<j} B_jm·h_m(new): each earlier row subtracted its new values at its end (below), in
+      // ascending m — the same operations in the same order as summing them here, so the same bits
       const double bjj = sB[j * k + j];
-      if (!(bjj > 0.0)) continue;  // unused component: row unchanged (oracle: same)
-      double bjm[4];
+      const int nsw = (int)nswp[j];
+      double hjv[2], bv[2], riv[2];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) bjm[m] = m < k ? sB[j * k + m] : 0.0;
+      for (int c = 0; c < 2; ++c) {
+        const int f = 2 * lane + c;
+        hjv[c] = f < F ? sH[j * F + f] : 0.0;
+        bv[c] = f < F ? bpre[j * F + f] : 0.0;
+        riv[c] = f < F ? rinvp[j * F + f] : 1.0;
+      }
+      double xnew[2] = {hjv[0], hjv[1]};  // an unused component (B_jj <= 0): row unchanged (oracle: same)
+      if (bjj > 0.0) {
 #ifdef CNMF_STAMPS
       const unsigned long long hs_t0 = __builtin_amdgcn_s_memtime();
+      const unsigned long long hs_r0 = __builtin_amdgcn_s_memrealtime();
       int hs_iters = 0;
       unsigned long long hs_ph[4] = {0, 0, 0, 0}, hs_m = hs_t0;
       auto hs_mark = [&](int ph) {
@@ -5149,23 +5205,19 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #else
 #define HS_MARK(p) ((void)0)
 #endif
-      // Jacobi (below) or the block PCR: decided per row from B_jj
-      const double rho = 10.0 * lam / bjj;
-      const bool jac = rho <= 0.05;
-      double rb[2], rd[2], re1[2], re2[2], xf[2];
+      // Jacobi (below) or the block PCR: decided per row from B_jj (the sweep count, precomputed)
+      const bool jac = nsw > 0;
+      double rb[2], rd[2], re1[2], re2[2], xf[2], rinv[2] = {1.0, 1.0};
       bool pas[2];
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         const int f = 2 * lane + c;
         rb[c] = 0.0; rd[c] = 1.0; re1[c] = 0.0; re2[c] = 0.0; xf[c] = 0.0;
         pas[c] = false;
-        const double hj = f < F ? sH[j * F + f] : 0.0;
+        const double hj = hjv[c];
         if (f < F) {
-          double b = sA[j * F + f];
-#pragma unroll
-          for (int m = 0; m < 4; ++m)
-            if (m < k && m != j) b -= bjm[m] * sH[m * F + f];
-          rb[c] = b;
+          rb[c] = bv[c];
+          rinv[c] = riv[c];
           rd[c] = bjj + ld0[c];
           re1[c] = le1[c];
           re2[c] = le2[c];
@@ -5186,11 +5238,12 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // all samples: ρ ~ 1e-4 at cfg5) sweeps from the warm start x = h_j reach the fp64 fixed
       // point in a few steps (bound: ρ^nsw <= 2^-55, and a sweep that changes no bit ends early) —
       // the same solve as the block PCR below at a fraction of its per-row cost.
-      int nsw = 0;
-      for (double r = 1.0; jac && r > 0x1p-55; r *= rho) ++nsw;
-      double rinv[2] = {1.0 / rd[0], 1.0 / rd[1]};
       HS_MARK(0);
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
+       // Jacobi: the KKT check from the last sweep's residuals r = b − (M − diag)·x (the sweep that
+       // changed no bit evaluates them at the final x): on P, x = r / M_ff < 0 iff r < 0; off P
+       // (x_f = 0) the dual y_f = (M x − b)_f = −r_f (past F, r = 0)
+       int cbad = 0;
        if (jac) {
         // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P); the neighbours
         // x[2l-2], x[2l-1] from lane l - 1 and x[2l+2], x[2l+3] from lane l + 1
@@ -5212,6 +5265,10 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           const bool chg = (x0 != xf[0]) || (x1 != xf[1]);
           xf[0] = x0;
           xf[1] = x1;
+          cbad = ((pas[0] ? r0 < 0.0 : r0 > 0.0) ? 1 : 0) | ((pas[1] ? r1 < 0.0 : r1 > 0.0) ? 2 : 0);
+#ifdef CNMF_STAMPS
+          hs_ph[1] += 1000ull;  // the stamps' "gather" slot counts the Jacobi sweeps (in thousands)
+#endif
           if (!__ballot(chg)) break;
         }
         HS_MARK(2);
@@ -5307,7 +5364,10 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
         // the KKT check: x >= 0 on P, the dual y = (M x − b)_f >= 0 off P (neighbours outside the
         // row enter with zero coefficients)
         bool bad[2];
-        {
+        if (jac) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) bad[c] = (cbad >> c) & 1;
+        } else {
           const double p0 = dpp_wave_shr(xf[0]), p1 = dpp_wave_shr(xf[1]);
           const double n0 = dpp_wave_shl(xf[0]), n1 = dpp_wave_shl(xf[1]);
           const double nm1[2] = {p1, xf[0]}, np1[2] = {xf[1], n0}, nm2[2] = {p0, p1}, np2[2] = {n0, n1};
@@ -5348,17 +5408,30 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
 #undef HS_MARK
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        if (2 * lane + c < F) sH[j * F + 2 * lane + c] = fmax(xf[c], 0.0);
+        xnew[c] = fmax(xf[c], 0.0);
+        if (2 * lane + c < F) sH[j * F + 2 * lane + c] = xnew[c];
       }
-      lds_order();
 #ifdef CNMF_STAMPS
-      if (lane == 0 && hs_call < 64u && j < 4) {
-        g_hs[(hs_call * 4 + j) * 2] = (unsigned long long)hs_iters;
+      if (lane == 0 && hs_call < 64u && j < 4) {  // BPP iterations | the row's 100 MHz ticks << 16
+        g_hs[(hs_call * 4 + j) * 2] = (unsigned long long)hs_iters | ((__builtin_amdgcn_s_memrealtime() - hs_r0) << 16);
         g_hs[(hs_call * 4 + j) * 2 + 1] = __builtin_amdgcn_s_memtime() - hs_t0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) g_hsp[(hs_call * 4 + j) * 4 + q] = hs_ph[q];
       }
 #endif
+      }
+      // the later rows' right-hand sides take this row's new values (each lane its own features:
+      // the later read is the same lane's, in order)
+#pragma unroll
+      for (int m = 1; m < 4; ++m)
+        if (m > j && m < k) {
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int f = 2 * lane + c;
+            if (f < F) bpre[m * F + f] -= sB[m * k + j] * xnew[c];
+          }
+        }
+      lds_order();
     }
   }
   __syncthreads();
@@ -7291,6 +7364,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   };
   auto end_iteration = [&](int it) {
     const bool last_it = it + 1 == a.n_iter;
+    // the thread's roles recomputed here from an opaque copy of its id (opaque_i)
+    const int t = opaque_i(threadIdx.x);
+    const int l = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int s4 = l & 3, g3 = l >> 2;
     // ---- end of this wave's iteration: mu_iter_wt_kernel's reduction (k = 4)
     if constexpr (MX) {
       // the quad's four sample groups summed (lanes 4·g3 .. 4·g3 + 3); its first lane writes the

@@ -15,6 +15,7 @@
 #                                      product library alternating n times -> <tag>_{base,prod}_r<i>.json
 #   timeline <tag> <args...>           tools/timeline_persist.py on the stamps build -> <tag>.log
 #   tlbase <tag> <args...>             the same on tools/ab/libcnmf_hip_base_stamps.so (A/B)
+#   tllib <tag> <lib> <args...>        the same on another stamps library file
 #   smoke                              __graft_entry__.smoke() -> smoke.log
 #   prof <tag> <bench.py args...>      rocprofv3 --kernel-trace --stats of a bench run -> <tag>/
 #   pmc <tag> "<counters>" <script args...>  one rocprofv3 --pmc pass over a python script -> <tag>/
@@ -44,6 +45,9 @@ for st in "$@"; do
       done ;;
     tlbase)  # the timeline on the base library's stamps build (same-box A/B of the timeline)
       CNMF_HIP_LIB=tools/ab/libcnmf_hip_base_stamps.so timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
+    tllib)
+      lib=$1; shift
+      CNMF_HIP_LIB=$lib timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     timeline)
       CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_stamps.so timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     smoke)

@@ -159,8 +159,13 @@ def main():
         _lib.check(fh(hb.ctypes.data), "hstep")
         hs = hb.reshape(64, 4, 2).astype(np.int64)
         used = hs[:, :, 1].sum(axis=1) > 0
-        summary["hstep_bpp_iters_per_row_last_calls"] = hs[used][-5:, :, 0].tolist()
+        it_ = hs[used][-5:, :, 0]
+        summary["hstep_bpp_iters_per_row_last_calls"] = (it_ & 0xFFFF).tolist()
         summary["hstep_kcycles_per_row_last_calls"] = (hs[used][-5:, :, 1] / 1e3).round(1).tolist()
+        rt = (it_ >> 16) * 10 / 1e3  # the one-wave form: the row's s_memrealtime ticks (100 MHz) above bit 16
+        if rt.max() > 0:
+            summary["hstep_us_per_row_last_calls"] = rt.round(2).tolist()
+            summary["hstep_shader_mhz"] = round(float(hs[used][-5:, :, 1].sum() / (rt.sum() * 1e3) * 1e3), 0)
         fp = getattr(lib, "cnmf_debug_hstep_phases", None)
         if fp is not None:  # the wave H-step's phases per row: setup, gather, PCR, check (k cycles)
             fp.argtypes = [ctypes.c_void_p]

@@ -256,6 +256,16 @@ __device__ unsigned long long g_stamps[16];
 // the end of a persistent bfw iteration: thread 0 of every workgroup sums the phase durations
 // (s_memtime) into g_eoi[slot]; g_eoi[15] counts the (workgroup, iteration) pairs
 __device__ unsigned long long g_eoi[16];
+// the persistent ALS resume path of workgroup 0: per slot the sum over iterations of the
+// s_memrealtime stamp (differences of the sums = summed phase durations); g_ph[15] counts
+__device__ unsigned long long g_ph[16];
+#define PH(slot)                                                                        \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x == 0) {                                          \
+      g_ph[slot] += __builtin_amdgcn_s_memrealtime();                                   \
+      if (slot == 0) g_ph[15] += 1ull;                                                  \
+    }                                                                                   \
+  } while (0)
 #define EOI_DECL unsigned long long eoi_t0 = 0;
 #define EOI(slot)                                                                     \
   do {                                                                                \
@@ -273,6 +283,7 @@ __device__ unsigned long long g_eoi[16];
 #define STAMP_FLUSH do {} while (0)
 #define EOI_DECL
 #define EOI(slot) do {} while (0)
+#define PH(slot) do {} while (0)
 #endif
 
 // ------------------------------------------------------------------------------------------------
@@ -5089,6 +5100,10 @@ __device__ __forceinline__ int opaque_i(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+__device__ __forceinline__ double opaque_d(double v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 
 // The same sweep for F <= 128 on ONE wave, without a workgroup barrier inside it (same LDS layout;
 // the other waves wait at the closing barrier).  Lane l holds features 2l and 2l + 1 (round 5: the
@@ -5147,6 +5162,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       nswp[t] = (double)nsw;
     }
     __syncthreads();
+    PH(3);
   }
   if (t < 64) {
     const int lane = t;
@@ -5435,6 +5451,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     }
   }
   __syncthreads();
+  PH(4);
 #ifdef CNMF_STAMPS
   if (t == 0 && blockIdx.x == 0) __hip_atomic_fetch_add(&g_hs_calls, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
@@ -6877,6 +6894,7 @@ __device__ __forceinline__ void wa_derive(unsigned char* smem, int t, double del
   for (int o = TPE / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   if (part == 0) sHHt[en] = v;
   __syncthreads();
+  PH(8);
   als_table(sHHt, K, K, delta2, reinterpret_cast<double*>(smem + L_TAB), t, TSTR);
   __syncthreads();
 }
@@ -6897,6 +6915,7 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
   }
   if (t < K * K) hB[t] = sAB[(t / K) * V + F + (t % K)];
   __syncthreads();
+  PH(2);
 #ifdef CNMF_ALS_NOHSTEP  // timing-only diagnostic: the persistent ALS without its H-step rows (H fixed)
   __syncthreads();
 #else
@@ -6904,7 +6923,9 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
 #endif
   for (int e = t; e < K * F; e += NT) sH[e] = hH[e];
   __syncthreads();
+  PH(5);
   wa_derive(smem, t, delta2);
+  PH(6);
 }
 
 // HREG (diagnostic A/B, one workgroup per CU): the lane's fp64 Hᵀ rows held in VGPRs for the
@@ -6992,6 +7013,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   if (TOL && t == 0) {
     sLoss[4] = ld_sc1(a.tolctl + TC_INIT);
     sLoss[5] = ld_sc1(a.tolctl + TC_PREV);
+    sLoss[6] = tolv;  // the test reads it from LDS (a register across the loop was spilled)
   }
   float* wsnap = nullptr;
   if (TOL) {
@@ -7228,7 +7250,9 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     }
     }  // the enumeration
     const float wn = (float)fmax(wn64, 0.0);
-    a.W[(size_t)tile * (16 * KK) + 4 * sm + gm] = wn;  // the tile's 256 contiguous bytes
+    // the tile's 256 contiguous bytes (the lane's offset opaque: TOL kept the 64-bit lane address
+    // across the iteration loop, spilled, and reloaded it behind a vmcnt(0) at every iteration)
+    a.W[(size_t)tile * (16 * KK) + opaque_i(4 * sm + gm)] = wn;
     // phase 3, regrouped: lane (s4 = l % 4, g3 = l / 4) takes the tile's samples 4j + s4 (j < 4) and
     // the features g3 + 16k (k < 6; k = 5 only for g3 = 0), x read again from the slot: 24 + 4 fp32
     // accumulators per lane instead of the (s, g) layout's 88 and no x registers across the FCLS —
@@ -7463,7 +7487,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
             sLoss[4] = sLoss[5] = errv;
             st_sc1(a.tolctl + TC_INIT, errv);
             st_sc1(a.tolctl + TC_PREV, errv);
-          } else if ((sLoss[5] - errv) / sLoss[4] < tolv) {
+          } else if ((sLoss[5] - errv) / sLoss[4] < sLoss[6]) {
             sFlag[3] = 1;
           } else {
             sLoss[5] = errv;
@@ -7506,6 +7530,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
         return;
       }
     }
+    if (!last_it) PH(0);
     // the basis state for the host (the last combiner of the launch, or the top of a stop)
     auto write_state = [&]() {
       for (int o = t; o < KK * wa::F; o += NT) a.H64[o] = sH[o];
@@ -7535,7 +7560,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       alive = false;
       if (!top) return;
       // the last combiner of the launch: the last H-step, then the basis state for the host
-      wa_update_basis(t, a.lam, a.delta2);
+      wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2));
       write_state();
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -7559,8 +7584,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
         sLoss[5] = errv;
       }
     }
-    wa_update_basis(t, a.lam, a.delta2);
+    PH(1);
+    wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2));
     load_h();
+    PH(7);
     TL(it, 1);
   };
 
@@ -7977,6 +8004,14 @@ int cnmf_debug_hstep(unsigned long long* host_out) {  // [64 calls][4 rows][BPP 
 }
 int cnmf_debug_hstep_phases(unsigned long long* host_out) {  // [64 calls][4 rows][4 phases] cycles
   HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_hsp), sizeof(unsigned long long) * 64 * 4 * 4));
+  return CNMF_OK;
+}
+int cnmf_debug_resume_phases(unsigned long long* host_out, int reset) {  // [16]: g_ph (PH)
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_ph), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_ph), z, sizeof(z)));
+  }
   return CNMF_OK;
 }
 int cnmf_debug_xtimeline(unsigned long long* host_out) {

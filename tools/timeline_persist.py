@@ -70,6 +70,11 @@ def main():
     assert plan.persistent
     plan.iterate(a.warmup)
     torch.cuda.synchronize()
+    fph = getattr(lib, "cnmf_debug_resume_phases", None)
+    if fph is not None:  # the ALS resume path's phase sums (workgroup 0), from this launch only
+        fph.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        fph.restype = ctypes.c_int
+        _lib.check(fph(np.zeros(16, dtype=np.uint64).ctypes.data, 1), "resume phases")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     plan.iterate(a.iters)
@@ -166,6 +171,20 @@ def main():
         if rt.max() > 0:
             summary["hstep_us_per_row_last_calls"] = rt.round(2).tolist()
             summary["hstep_shader_mhz"] = round(float(hs[used][-5:, :, 1].sum() / (rt.sum() * 1e3) * 1e3), 0)
+        if fph is not None:
+            pb = np.zeros(16, dtype=np.uint64)
+            _lib.check(fph(pb.ctypes.data, 0), "resume phases")
+            cnt = int(pb[15])
+            if cnt:
+                # the stamps in time order (slot 8: the derive's Hᵀ / HHᵀ done, before the table)
+                order = [0, 1, 2, 3, 4, 5, 8, 6, 7]
+                names = ["poll_to_AB_in_LDS", "AB_to_copies", "phaseA", "rows", "H_back", "Ht_HHt", "table",
+                         "load_h"]
+                sums = pb.astype(np.int64)
+                summary["resume_phases_us_wg0"] = {
+                    names[i]: round(float(sums[order[i + 1]] - sums[order[i]]) / cnt * 10 / 1e3, 3)
+                    for i in range(len(names)) if sums[order[i + 1]] and sums[order[i]]}
+                summary["resume_phases_n"] = cnt
         fp = getattr(lib, "cnmf_debug_hstep_phases", None)
         if fp is not None:  # the wave H-step's phases per row: setup, gather, PCR, check (k cycles)
             fp.argtypes = [ctypes.c_void_p]

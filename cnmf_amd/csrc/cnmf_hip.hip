@@ -5463,73 +5463,79 @@ __device__ __forceinline__ void als_hstep(unsigned char* smem, int F, int k, dou
   else als_hstep_block(smem, F, k, lam, t);
 }
 
-// The W-step's passive-set table from HHᵀ (stride KP): per mask (thread t < 16) the inverse of
-// Q_PP, Q = HHᵀ + δ²11ᵀ, by Gauss-Jordan with partial pivoting, scattered to 4x4, and the valid flag
+// The W-step's passive-set table from HHᵀ (stride KP): per mask P the inverse of Q_PP,
+// Q = HHᵀ + δ²11ᵀ, by Gauss-Jordan with partial pivoting, scattered to 4x4, and the valid flag.
+// One wave, lane L = 4·mask + r holding row r of the 4x8 [Q | I] (rows / columns outside P at the
+// identity): every lane eliminates its own row, so a pivot step is ~70 instructions for all 16
+// masks instead of ~150 for one mask per lane (round 5: 1.9 -> ~0.5 µs of the ALS resume).  Rows
+// are not moved: each lane carries its row's position, and a swap of positions c and piv only swaps
+// the two lanes' position numbers.  The arithmetic is the row-per-thread form's, operation for
+// operation: the pivot is the largest |a[pos][c]| over P's positions >= c, the first position on ties
+// (the ascending strict-> search), the pivot row scaled by 1 / a[c][c], every other P row updated
+// a[e] -= a[c] · pivot[e] — so the table is the same bits.
 __device__ void als_table(const double* HHt, int KP, int k, double delta2, double* table, int t, int mstride = 16) {
-  // Register-resident form (every index compile-time; the runtime-indexed compressed arrays went to
-  // scratch): Gauss-Jordan on the full 4x4 [Q | I] with the rows / columns outside P held at the
-  // identity.  The entries of P see exactly the compressed elimination's operations in the same
-  // order (the pivot search runs over P's rows in ascending order, strict >, as the compressed
-  // search does; rows outside P are never touched by an elimination step of a P column and vice
-  // versa), so the table is the same bits as the compressed form's.
-  if (t < 16) {
-    const int mask = t;
+  if (t < 64) {
+    const int mask = t >> 2, r0 = t & 3;
+    const int qb = t & ~3;  // the quad's first lane
     bool valid = !(k < 4 && (mask >> k) != 0);
-    double a[4][8];
+    double a[8];
     double dmax = 0.0;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bool in = (mask >> r & 1) && (mask >> c & 1);
-        const double q = (r < k && c < k) ? HHt[r * KP + c] + delta2 : 0.0;
-        a[r][c] = in ? q : (r == c ? 1.0 : 0.0);
-        a[r][4 + c] = r == c ? 1.0 : 0.0;
-        if (in && r == c) dmax = fmax(dmax, fabs(q));
-      }
+    for (int c = 0; c < 4; ++c) {
+      const bool in = (mask >> r0 & 1) && (mask >> c & 1);
+      const double q = (r0 < k && c < k) ? HHt[r0 * KP + c] + delta2 : 0.0;
+      a[c] = in ? q : (r0 == c ? 1.0 : 0.0);
+      a[4 + c] = r0 == c ? 1.0 : 0.0;
+      if (in && r0 == c) dmax = fabs(q);
+    }
+    dmax = fmax(dmax, wt::dpp64<0xB1>(dmax));  // the quad's largest P diagonal (max: exact in any order)
+    dmax = fmax(dmax, wt::dpp64<0x4E>(dmax));
+    int pos = r0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      if (!(mask >> c & 1)) continue;  // identity column: nothing to eliminate
-      // pivot: the P row r >= c of largest |a[r][c]| (first on ties)
-      int piv = c;
-      double pv = fabs(a[c][c]);
+      if (!(mask >> c & 1)) continue;  // identity column: nothing to eliminate (quad-uniform)
+      const bool inp = (mask >> pos & 1) != 0;
+      // the pivot: (|a[c]|, position) maximised lexicographically with the smaller position winning
+      // ties, over P's positions >= c (position c always qualifies)
+      double pv = (inp && pos >= c) ? fabs(a[c]) : -1.0;
+      int pp = pos;
 #pragma unroll
-      for (int r = c + 1; r < 4; ++r) {
-        const bool take = (mask >> r & 1) && fabs(a[r][c]) > pv;
-        piv = take ? r : piv;
-        pv = take ? fabs(a[r][c]) : pv;
+      for (int x = 0; x < 2; ++x) {
+        const double ov = x == 0 ? wt::dpp64<0xB1>(pv) : wt::dpp64<0x4E>(pv);
+        const int op = x == 0 ? __builtin_amdgcn_update_dpp(0, pp, 0xB1, 0xF, 0xF, true)
+                              : __builtin_amdgcn_update_dpp(0, pp, 0x4E, 0xF, 0xF, true);
+        const bool tk = ov > pv || (ov == pv && op < pp);
+        pv = tk ? ov : pv;
+        pp = tk ? op : pp;
       }
       valid = valid && pv > 1e-13 * dmax;
-      // swap rows c and piv (selects)
+      // swap positions c and pp (position numbers only)
+      const int npos = pos == pp ? c : (pos == c ? pp : pos);
+      pos = npos;
+      const bool piv = pos == c;
+      if (piv) {
+        const double inv = 1.0 / a[c];
 #pragma unroll
-      for (int r = c + 1; r < 4; ++r) {
-        const bool sw = piv == r;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const double tc = a[c][e], tr = a[r][e];
-          a[c][e] = sw ? tr : tc;
-          a[r][e] = sw ? tc : tr;
-        }
+        for (int e = 0; e < 8; ++e) a[e] *= inv;
       }
-      const double inv = 1.0 / a[c][c];
+      // the pivot row to the quad: its lane is the one now at position c
+      const unsigned long long pb = __ballot(piv);
+      const int src = qb + (int)__builtin_ctzll((pb >> qb) & 0xFull);
+      double pr[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) a[c][e] *= inv;
+      for (int e = 0; e < 8; ++e) pr[e] = __shfl(a[e], src, 64);
+      if (!piv && (mask >> pos & 1)) {
+        const double fct = a[c];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (r == c || !(mask >> r & 1)) continue;
-        const double fct = a[r][c];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[r][e] -= fct * a[c][e];
+        for (int e = 0; e < 8; ++e) a[e] -= fct * pr[e];
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bool in = (mask >> r & 1) && (mask >> c & 1);
-        table[mask * mstride + r * 4 + c] = (valid && in) ? a[r][4 + c] : 0.0;
-      }
-    table[16 * mstride + mask] = valid ? 1.0 : 0.0;
+    for (int c = 0; c < 4; ++c) {
+      const bool in = (mask >> pos & 1) && (mask >> c & 1);
+      table[mask * mstride + pos * 4 + c] = (valid && in) ? a[4 + c] : 0.0;
+    }
+    if (r0 == 0) table[16 * mstride + mask] = valid ? 1.0 : 0.0;
   }
 }
 
@@ -6835,8 +6841,7 @@ constexpr int K = 4, NL = 4, TSW = 16, F = wt::F, NQ = G4::NQ, V = F + K, NOUT =
 constexpr int NACC = G4::NACC;                                  // NQ·K + K fp32 accumulators
 constexpr int L_STG = 0;                                        // [NWV][XSTR]
 constexpr int L_RED = L_STG + wt::NWV * G4::XSTR;               // [NWV][NL][NACC] fp32
-constexpr int L_H = L_RED + wt::NWV * NL * NACC * 4;            // H fp64 [K][F]
-constexpr int L_AB = L_H + K * F * 8;                           // AB fp64 [K][V]
+constexpr int L_AB = L_RED + wt::NWV * NL * NACC * 4;           // AB fp64 [K][V] (the top's sum; TOL: + loss)
 constexpr int L_HT = L_AB + (NOUT + 2) * 8;                     // Hᵀ fp64 [NL·NQ][K], rows >= F zero
 constexpr int L_HHT = L_HT + NL * NQ * K * 8;                   // HHᵀ fp64 [K][K]
 // passive-set table, masks at a stride of TSTR doubles (18: the four masks a quad reads with one
@@ -6848,6 +6853,7 @@ constexpr int L_LOSS = (L_FLAG + 16 + 15) / 16 * 16;            // TOL: [NWV] wa
 constexpr int L_WSTG = L_LOSS + 8 * 8;                          // TOL: [NWV] the old W tile (256 B)
 constexpr int L_LACC = L_WSTG + wt::NWV * 256;                  // TOL: [NWV][64] the lanes' loss sums
 constexpr int L_HS = L_LACC + wt::NWV * 64 * 8;                 // als_hstep's arrays (als_lds_bytes)
+constexpr int L_H = L_HS + K * F * 8;                           // H fp64 [K][F]: the H-step's own sH
 static_assert(L_RED % 16 == 0 && L_HT % 16 == 0 && L_HS % 16 == 0, "16-byte aligned LDS regions");
 static_assert(NOUT * 8 >= wt::NWV * 64 * 4, "the prologue's dummy stores stay inside the partial row");
 }  // namespace wa
@@ -6899,21 +6905,20 @@ __device__ __forceinline__ void wa_derive(unsigned char* smem, int t, double del
   __syncthreads();
 }
 
-// the H-step on AB in LDS: one Gauss-Seidel sweep of exact NNLS rows (als_hstep), then wa_derive
+// The H-step: AB is in the H-step's A / B arrays already (the workgroups that load it scatter it
+// there; copy_ab: the top combiner's sum, from sAB) and H is the H-step's own sH (no copies in or
+// out: 0.4 + 0.3 µs).  One Gauss-Seidel sweep of exact NNLS rows (als_hstep), then wa_derive
 // (inlined once, after the kernel's streaming loop)
-__device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2) {
+__device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2, bool copy_ab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   using namespace wa;
-  double* sH = reinterpret_cast<double*>(smem + L_H);
   const double* sAB = reinterpret_cast<const double*>(smem + L_AB);
   double* hA = reinterpret_cast<double*>(smem + L_HS);
-  double* hH = hA + K * F;
-  double* hB = hH + K * F;
-  for (int e = t; e < K * F; e += NT) {
-    hA[e] = sAB[(e / F) * V + (e % F)];
-    hH[e] = sH[e];
+  double* hB = hA + 2 * K * F;
+  if (copy_ab) {
+    for (int e = t; e < K * F; e += NT) hA[e] = sAB[(e / F) * V + (e % F)];
+    if (t < K * K) hB[t] = sAB[(t / K) * V + F + (t % K)];
   }
-  if (t < K * K) hB[t] = sAB[(t / K) * V + F + (t % K)];
   __syncthreads();
   PH(2);
 #ifdef CNMF_ALS_NOHSTEP  // timing-only diagnostic: the persistent ALS without its H-step rows (H fixed)
@@ -6921,8 +6926,6 @@ __device__ __forceinline__ void wa_update_basis(int t, double lam, double delta2
 #else
   als_hstep(smem + L_HS, F, K, lam, t);
 #endif
-  for (int e = t; e < K * F; e += NT) sH[e] = hH[e];
-  __syncthreads();
   PH(5);
   wa_derive(smem, t, delta2);
   PH(6);
@@ -7560,7 +7563,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       alive = false;
       if (!top) return;
       // the last combiner of the launch: the last H-step, then the basis state for the host
-      wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2));
+      wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2), true);
       write_state();
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -7576,7 +7579,15 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       return;
     }
     if (!top) {
-      for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      // AB straight into the H-step's A / B arrays (TOL's loss slot into sAB)
+      double* hA = reinterpret_cast<double*>(smem + wa::L_HS);
+      for (int o = t; o < NOUTT; o += NT) {
+        const double v = ld_sc1(a.AB + o);
+        const int j = o / V, c = o - j * V;
+        if (o >= NOUT) sAB[o] = v;
+        else if (c < wa::F) hA[j * wa::F + c] = v;
+        else hA[2 * KK * wa::F + j * KK + (c - wa::F)] = v;
+      }
       __syncthreads();
       if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
         const double errv = sqrt(fmax(sAB[NOUT], 0.0));
@@ -7585,7 +7596,7 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       }
     }
     PH(1);
-    wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2));
+    wa_update_basis(t, opaque_d(a.lam), opaque_d(a.delta2), top);
     load_h();
     PH(7);
     TL(it, 1);

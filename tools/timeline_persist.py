@@ -176,14 +176,13 @@ def main():
             _lib.check(fph(pb.ctypes.data, 0), "resume phases")
             cnt = int(pb[15])
             if cnt:
-                # the stamps in time order (slot 8: the derive's Hᵀ / HHᵀ done, before the table)
-                order = [0, 1, 2, 3, 4, 5, 8, 6, 7]
-                names = ["poll_to_AB_in_LDS", "AB_to_copies", "phaseA", "rows", "H_back", "Ht_HHt", "table",
-                         "load_h"]
+                # the stamps present, in time order (cnmf_hip.hip PH(slot)): 0 flag seen, 1 AB in LDS,
+                # 2 barrier, 3 (unused), 4 rows done, 5 after the H-step, 6 table done, 7 basis ready
                 sums = pb.astype(np.int64)
+                present = [q for q in range(8) if sums[q] > 0]
                 summary["resume_phases_us_wg0"] = {
-                    names[i]: round(float(sums[order[i + 1]] - sums[order[i]]) / cnt * 10 / 1e3, 3)
-                    for i in range(len(names)) if sums[order[i + 1]] and sums[order[i]]}
+                    f"{a_}->{b_}": round(float(sums[b_] - sums[a_]) / cnt * 10 / 1e3, 3)
+                    for a_, b_ in zip(present, present[1:])}
                 summary["resume_phases_n"] = cnt
         fp = getattr(lib, "cnmf_debug_hstep_phases", None)
         if fp is not None:  # the wave H-step's phases per row: setup, gather, PCR, check (k cycles)

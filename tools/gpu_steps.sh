@@ -20,6 +20,7 @@
 #   prof <tag> <bench.py args...>      rocprofv3 --kernel-trace --stats of a bench run -> <tag>/
 #   pmc <tag> "<counters>" <script args...>  one rocprofv3 --pmc pass over a python script -> <tag>/
 #   py <tag> <script args...>          python <script> -> <tag>.log
+#   pylib <tag> <lib> <script args...> the same with CNMF_HIP_LIB=<lib>
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 D=gpurun_out/$1; shift; mkdir -p "$D"
@@ -59,6 +60,9 @@ for st in "$@"; do
       ctrs=${1//,/ }; shift
       mkdir -p "$D/$tag"
       timeout -s KILL 120 rocprofv3 --pmc $ctrs -d "$D/$tag" -o run -- python3 -u "$@" > "$D/$tag/out.log" 2>&1 || { tail -20 "$D/$tag/out.log"; exit 1; } ;;
+    pylib)
+      lib=$1; shift
+      CNMF_HIP_LIB=$lib timeout -k 10 400 python -u "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     py)
       timeout -k 10 400 python -u "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     *) echo "unknown step $kind"; exit 2 ;;

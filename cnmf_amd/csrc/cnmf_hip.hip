@@ -3804,7 +3804,11 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   const int nbt_max = (int)((a.n_tiles + NW - 1) / NW);
   unsigned char* stg = smem + G_::L_STG + w * XSTR;
   unsigned char* wstg = smem + G_::L_WSTG + w * WBW;  // streamed W: this wave's current tile
-  float* wres = reinterpret_cast<float*>(smem + G_::L_WRES + (size_t)w * nbt_max * WBW);  // [i][TSW][K]
+  // W streamed: its first nres tiles per wave resident all the same (the LDS the plan has left; round
+  // 5): their W loads re-load an X chunk (the counted waits see the same loads) and their stores go
+  // to the dummy word (the same stores), the rest streams
+  const int nres = WRES ? 0 : __builtin_amdgcn_readfirstlane(a.n_static);
+  float* wres = reinterpret_cast<float*>(smem + G_::L_WRES + (size_t)w * (WRES ? nbt_max : nres) * WBW);  // [i][TSW][K]
   float* red = reinterpret_cast<float*>(smem + G_::L_RED);
   double* sH = reinterpret_cast<double*>(smem + G_::L_H);
   double* sAB = reinterpret_cast<double*>(smem + G_::L_AB);
@@ -3837,12 +3841,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   if (a.apply_first)
     for (int i = t; i < NOUT; i += NT) sAB[i] = a.AB[i];
   if (l < G_::PADB / 4) reinterpret_cast<float*>(stg + XBW)[l] = 0.f;
-  if (WRES)
-    for (int c = l; c < nbt * (WBW / 16); c += 64) {
+  {
+    const int nw = WRES ? nbt : min(nres, nbt);
+    for (int c = l; c < nw * (WBW / 16); c += 64) {
       const int i = c / (WBW / 16), ch = c - i * (WBW / 16);
       *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(wres) + i * WBW + 16 * ch) =
           *reinterpret_cast<const u32x4*>(Wb + (size_t)(gw + (int64_t)NW * i) * WBW + 16 * ch);
     }
+  }
   __syncthreads();
   if (a.apply_first)
     wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
@@ -3885,7 +3891,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // the tile's 16-byte chunks of this lane: l + 64u (u < PFW - 1) and, for lanes < LASTL, the last
   // (other lanes re-load chunk l: never staged; every lane issues the same loads), then the W tile
   // when streamed (lanes < 16; others re-load chunk l)
-  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile) {
+  auto prefetch = [&](u32x4 (&pf)[PFS], int64_t tile, int ti) {
 #ifdef CNMF_DIAG_L2
     const unsigned char* xs = Xb + (size_t)(tile & 255) * XBW + 16 * l;
 #else
@@ -3894,7 +3900,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
 #pragma unroll
     for (int u = 0; u < PFW - 1; ++u) ld16(pf[u], xs + 1024 * u);
     ld16(pf[PFW - 1], l < LASTL ? xs + 1024 * (PFW - 1) : xs);
-    if (!WRES) ld16(pf[PFW], l < WBW / 16 ? Wb + (size_t)tile * WBW + 16 * l : xs);
+    if (!WRES) ld16(pf[PFW], (l < WBW / 16 && ti >= nres) ? Wb + (size_t)tile * WBW + 16 * l : xs);
   };
   auto stage = [&](const u32x4 (&pf)[PFS]) {
     const unsigned addr = (unsigned)(uintptr_t)(stg + 16 * l);
@@ -3913,7 +3919,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
-    prefetch(pf[k], gw + (int64_t)NW * k);  // the host keeps nbt > PD
+    prefetch(pf[k], gw + (int64_t)NW * k, k);  // the host keeps nbt > PD
 #pragma unroll
     for (int d = 0; d < NSTB; ++d) asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
   }
@@ -3934,7 +3940,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     // TOL the snapshot store every body issues (a loss iteration's W, else a dummy)
     wait_set<PFS * (PD - 1) + NSTB * PD, PFS>(pfk);
     stage(pfk);
-    prefetch(pfk, gw + (int64_t)NW * nx_i);
+    prefetch(pfk, gw + (int64_t)NW * nx_i, nx_i);
     if (++nx_i == nbt) nx_i = 0;
   };
   auto body = [&]() {
@@ -4018,7 +4024,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       num = keep + dpp64<0xB1>(send);  // quad_perm [1,0,3,2]
     }
     // phase 2: w[s][e] <- w·num/den (SK:553-629)
-    float* wt_ = WRES ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);
+    const bool wr = WRES || i < nres;  // this tile's W resident
+    float* wt_ = wr ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);
     float wv[KK];
 #pragma unroll
     for (int m4 = 0; m4 < KK / 4; ++m4) {
@@ -4072,7 +4079,10 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     if (den == 0.0) den = EPS32;                // SK:620
     const float wn = (float)(wold * div_nr(num, den));  // SK:622-629
     wt_[s * KK + e] = wn;
-    if (!WRES) reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wn;  // lane l = (s, e)
+    if (!WRES) {  // lane l = (s, e); a resident tile's store goes to the dummy word
+      if (!wr) reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wn;
+      else asm volatile("global_store_dword %0, %1, off" ::"v"(dummy), "v"(0) : "memory");
+    }
     // w'[s][·]: the sample's row back from LDS (this wave's writes above precede the reads)
     f2 wp[KP];
 #pragma unroll
@@ -4248,8 +4258,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     if (last_it) {
       alive = false;
-      if (WRES)  // this wave's W back to HBM, once per launch
-        for (int c = l; c < nbt * (WBW / 16); c += 64) {
+      if (WRES || nres > 0)  // this wave's resident W back to HBM, once per launch
+        for (int c = l; c < (WRES ? nbt : min(nres, nbt)) * (WBW / 16); c += 64) {
           const int ii = c / (WBW / 16), ch = c - ii * (WBW / 16);
           *reinterpret_cast<u32x4*>(Wb + (size_t)(gw + (int64_t)NW * ii) * WBW + 16 * ch) =
               *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(wres) + ii * WBW + 16 * ch);
@@ -5872,8 +5882,10 @@ static int64_t max_resident(PassFn fn, size_t lds) {
     auto it = g_occ.find(key);
     if (it != g_occ.end()) return it->second;
   }
+  // the function's LDS ceiling at the chip's maximum, not at this plan's size: a later plan of the
+  // same kernel with a smaller (cached) size must not lower it under an earlier, larger one
   if (lds > 64 * 1024)
-    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds) != hipSuccess)
       return -1;
   int per_cu = 0, ncu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds) != hipSuccess) return -1;
@@ -8207,11 +8219,14 @@ static int64_t persist_teams_grid(int64_t n_tiles, bool multi, int layout, size_
 // ---- variant 4: barrier-free wave tiles (mu_iter_wt_kernel<K, WRES, PD, MULTI>: one 4-wave
 // workgroup per CU, each wave on its own tiles; fp32 X, F = 81, k = 4 (16-sample tiles) or k = 8
 // (8-sample tiles); W resident in LDS when the grid's share fits, else streamed with X).
-// CNMF_WT_PD = prefetch depth 2..4 of the k = 4 W-resident single-GPU kernel (default 3).
+// CNMF_WT_PD = prefetch depth 2..4 of the k = 4 W-resident single-GPU kernel, 3..5 of the k = 8
+// streamed-W one (default 3).
 static int wt_pd(int k, bool wres, bool multi) {
   const char* v = diag_env("CNMF_WT_PD");
   const int pd = v ? atoi(v) : 3;
-  return (k == 4 && wres && !multi && pd >= 2 && pd <= 4) ? pd : 3;
+  if (k == 4 && wres && !multi && pd >= 2 && pd <= 4) return pd;
+  if (k == 8 && !wres && !multi && pd >= 3 && pd <= 5) return pd;
+  return 3;
 }
 extern "C++" {
 template <int KK, bool WRES>
@@ -8222,6 +8237,8 @@ static PassFn wt_fn_k(int pd, bool multi, bool tol) {
   if (multi) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true>);
   if (KK == 4 && WRES && pd == 2) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 2, false>);
   if (KK == 4 && WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 4, false>);
+  if (KK == 8 && !WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<8, false, 4, false>);
+  if (KK == 8 && !WRES && pd == 5) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<8, false, 5, false>);
   return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false>);
 }
 }
@@ -8252,7 +8269,9 @@ struct WtLaunch {
   PassFn fn;
   int64_t G, n_tiles;
   size_t lds;
-  bool mf;  // k = 8 on the matrix cores (mu_iter_mf8_kernel)
+  bool mf;       // k = 8 on the matrix cores (mu_iter_mf8_kernel)
+  int nres = 0;  // W streamed: the first nres tiles of every wave resident in the LDS left over
+  bool wres = false;  // W resident (every tile)
 };
 // the wave-tile launch for this shape, or false (not eligible: another kernel serves it).  k = 4
 // follows the layout switch (variant 4, the default); k = 8 has no other persistent layout.
@@ -8281,11 +8300,21 @@ static bool wt_plan(int64_t n_rows, int x_dtype, int F, int k, bool multi, int l
     const int64_t nbt_max = (n_tiles + wt::NWV * G - 1) / (wt::NWV * G);
     // W resident: the four waves' W tiles; TOL (the wave-tile kernel) a second copy: the snapshot of
     // the checked state
-    const size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw * (tol && !mf ? 2 : 1) : 0);
+    size_t lds = l_wres + (wres ? (size_t)wt::NWV * nbt_max * wbw * (tol && !mf ? 2 : 1) : 0);
     if (lds > kMaxLds) continue;
+    // W streamed (the VALU wave tiles): as many of each wave's tiles W-resident as the LDS holds —
+    // their W neither read nor written through HBM in the iterations (cfg3's shard: ~78 % of its W
+    // traffic).  CNMF_WT_NRES (diagnostic) caps it; 0 streams every tile.
+    int nres = 0;
+    if (!wres && !mf) {
+      int64_t cap = (int64_t)((kMaxLds - lds) / ((size_t)wt::NWV * wbw));
+      if (const char* nr = diag_env("CNMF_WT_NRES")) cap = std::min<int64_t>(cap, atoi(nr));
+      nres = (int)std::max<int64_t>(0, std::min<int64_t>(cap, nbt_max));
+      lds += (size_t)wt::NWV * nres * wbw;
+    }
     const PassFn fn = mf ? mf8_fn(wres != 0, multi, tol) : wt_fn(k, wres != 0, multi, tol);
     if (max_resident(fn, lds) < G) continue;  // the whole grid co-resident (cached query)
-    *out = WtLaunch{fn, G, n_tiles, lds, mf};
+    *out = WtLaunch{fn, G, n_tiles, lds, mf, nres, wres != 0};
     return true;
   }
   return false;
@@ -8497,7 +8526,7 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.n_groups = (int)((L.G + sl::GROUP - 1) / sl::GROUP);
   if (const char* gz = diag_env("CNMF_WT_GROUP"))  // diagnostic: workgroups per first-level group
     if (atoi(gz) > 0) pa.n_groups = (int)std::min<int64_t>((L.G + atoi(gz) - 1) / atoi(gz), sl::MAX_GROUPS);
-  pa.n_static = 0;
+  pa.n_static = L.nres;
   pa.l1W = l1_W;
   pa.l2W = l2_W;
   pa.l1H = l1_H;
@@ -8535,19 +8564,22 @@ int cnmf_persist_describe(int64_t n_rows, int n_features, int k, int x_dtype, in
   RESOLVE_LAYOUT(layout);
   WtLaunch L;
   if (wt_plan(n_rows, x_dtype, n_features, k, false, layout, &L)) {
-    const bool wres = L.lds > (L.mf ? (size_t)wt::GeoMF8::L_WRES
-                                    : (k == 4 ? (size_t)wt::Geo<4>::L_WRES : (size_t)wt::Geo<8>::L_WRES));
+    const bool wres = L.wres;
+    char wdesc[96];
+    if (wres) snprintf(wdesc, sizeof wdesc, "resident in LDS");
+    else if (L.nres > 0) snprintf(wdesc, sizeof wdesc, "streamed with X but for %d tiles per wave resident in LDS", L.nres);
+    else snprintf(wdesc, sizeof wdesc, "streamed with X");
     if (L.mf)
       snprintf(out, (size_t)len,
                "mu_iter_mf8_kernel<k=8, W %s, PD=3>: matrix-core wave tiles of 16 samples "
                "(v_mfma_f32_16x16x4_f32), one 4-wave workgroup per CU (%lld workgroups), no barrier inside "
                "an iteration",
-               wres ? "resident in LDS" : "streamed with X", (long long)L.G);
+               wdesc, (long long)L.G);
     else
       snprintf(out, (size_t)len,
                "mu_iter_wt_kernel<k=%d, W %s, PD=%d>: wave tiles of %d samples, one 4-wave workgroup per CU "
                "(%lld workgroups), no barrier inside an iteration",
-               k, wres ? "resident in LDS" : "streamed with X", wt_pd(k, wres, false), 64 / k, (long long)L.G);
+               k, wdesc, wt_pd(k, wres, false), 64 / k, (long long)L.G);
     return 1;
   }
   BwpLaunch B;

@@ -3956,6 +3956,40 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     const bool loss_it = TOL && ((it0 + it) % 10 == 0);  // check the state after it0 + it iterations
 #endif
     const int64_t tile = gw + (int64_t)NW * i;
+    // phase 2 first where it does not need x: the sample's W row and den = w·HHᵀ[e] with its refined
+    // reciprocal (div_nr's v_rcp_f64 + Newton step, so w·num·r is div_nr's arithmetic) — their loads
+    // and their ~15-deep dependent chain then overlap phase 1 instead of following the reduce-scatter
+    // (round 5).  SK:553-629
+    const bool wr = WRES || i < nres;  // this tile's W resident
+    float* wt_ = wr ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);
+    float wv[KK];
+#pragma unroll
+    for (int m4 = 0; m4 < KK / 4; ++m4) {
+      const float4 v4 = *reinterpret_cast<const float4*>(wt_ + s * KK + 4 * m4);
+      wv[4 * m4] = v4.x;
+      wv[4 * m4 + 1] = v4.y;
+      wv[4 * m4 + 2] = v4.z;
+      wv[4 * m4 + 3] = v4.w;
+    }
+    const float wold32 = wt_[s * KK + e];
+    const double wold = (double)wold32;
+    double den = 0.0;
+    if constexpr (KK == 8) {
+      // den = w·HHᵀ[e] in packed fp32 (8 positive terms: no cancellation, ≤ 8 roundings), the
+      // update itself in fp64
+      f2 d2 = f2{0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < KP; ++q) d2 = __builtin_elementwise_fma(f2{wv[2 * q], wv[2 * q + 1]}, hh32[q], d2);
+      den = (double)(d2.x + d2.y);
+    } else {
+#pragma unroll
+      for (int m = 0; m < KK; ++m) den = fma((double)wv[m], hh[m], den);
+    }
+    if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
+    if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
+    if (den == 0.0) den = EPS32;                // SK:620
+    double rden = __builtin_amdgcn_rcp(den);
+    rden = fma(rden, fma(-den, rden, 1.0), rden);
     // phase 1: x along the lane's row, packed fp32 chains of 7 features folded into fp64
     const float* xr = reinterpret_cast<const float*>(stg) + s * F + NQ * e;
     float xv[NQ];
@@ -4023,20 +4057,6 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       const double keep = b1 ? k2[1] : k2[0], send = b1 ? k2[0] : k2[1];
       num = keep + dpp64<0xB1>(send);  // quad_perm [1,0,3,2]
     }
-    // phase 2: w[s][e] <- w·num/den (SK:553-629)
-    const bool wr = WRES || i < nres;  // this tile's W resident
-    float* wt_ = wr ? wres + i * (TSW * KK) : reinterpret_cast<float*>(wstg);
-    float wv[KK];
-#pragma unroll
-    for (int m4 = 0; m4 < KK / 4; ++m4) {
-      const float4 v4 = *reinterpret_cast<const float4*>(wt_ + s * KK + 4 * m4);
-      wv[4 * m4] = v4.x;
-      wv[4 * m4 + 1] = v4.y;
-      wv[4 * m4 + 2] = v4.z;
-      wv[4 * m4 + 3] = v4.w;
-    }
-    const float wold32 = wt_[s * KK + e];
-    const double wold = (double)wold32;
     if constexpr (TOL && WRES) {
       // the W of the state a loss iteration checks, kept in LDS (written to HBM only on a stop)
       if (loss_it) wsnapl[i * (TSW * KK) + s * KK + e] = wold32;
@@ -4062,22 +4082,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       lossacc += (double)l2;
     }
-    double den = 0.0;
-    if constexpr (KK == 8) {
-      // den = w·HHᵀ[e] in packed fp32 (8 positive terms: no cancellation, ≤ 8 roundings), the
-      // update itself in fp64
-      f2 d2 = f2{0.f, 0.f};
-#pragma unroll
-      for (int q = 0; q < KP; ++q) d2 = __builtin_elementwise_fma(f2{wv[2 * q], wv[2 * q + 1]}, hh32[q], d2);
-      den = (double)(d2.x + d2.y);
-    } else {
-#pragma unroll
-      for (int m = 0; m < KK; ++m) den = fma((double)wv[m], hh[m], den);
-    }
-    if (a.l1W > 0.0) den += a.l1W;              // SK:616-617
-    if (a.l2W > 0.0) den = den + a.l2W * wold;  // SK:618-619
-    if (den == 0.0) den = EPS32;                // SK:620
-    const float wn = (float)(wold * div_nr(num, den));  // SK:622-629
+    const float wn = (float)(wold * (num * rden));  // SK:622-629 (div_nr's arithmetic)
     wt_[s * KK + e] = wn;
     if (!WRES) {  // lane l = (s, e); a resident tile's store goes to the dummy word
       if (!wr) reinterpret_cast<float*>(Wb)[(size_t)tile * TSW * KK + l] = wn;

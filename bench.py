@@ -305,14 +305,15 @@ def clock_ramp(plan, seconds: float, world: int, dev, sync, trip: int = 100) -> 
     return el, trips
 
 
-def load_traffic(path, n_rows, F, k):
-    """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py)."""
+def load_traffic(path, n_rows, F, k, variant=""):
+    """PMC-measured HBM bytes of ONE iteration of the dominant kernel (tools/pmc_traffic.py), keyed by
+    the shape and the solver variant ("_als", "_w" for the weighted MU, "" for the MU)."""
     try:
         with open(path) as f:
             d = json.load(f)
     except Exception:
         return None, None
-    key = f"{n_rows}x{F}_k{k}"
+    key = f"{n_rows}x{F}_k{k}{variant}"
     ent = d.get(key)
     if not ent:
         return None, None
@@ -718,7 +719,8 @@ def main():
     achieved = bytes_per_launch / avg_pass_s_max / 1e9
     layout = res["layout"]
 
-    traffic, traffic_src = (None, None) if (args.solver == "als" or args.weighted) else load_traffic(args.traffic_json, n_rows, F, k)
+    variant = "_als" if args.solver == "als" else ("_w" if args.weighted else "")
+    traffic, traffic_src = load_traffic(args.traffic_json, n_rows, F, k, variant)
     if traffic is not None:
         traffic = traffic * iters_per_launch
     if args.weighted and persistent:

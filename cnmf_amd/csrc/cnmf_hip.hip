@@ -5267,7 +5267,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // |1, −4, −4, 1| of DᵀD) against a diagonal >= B_jj, so ρ = 10λ / B_jj bounds the Jacobi
       // contraction of any passive subsystem M_PP in the max norm.  At ρ <= 1/20 (B_jj is a sum over
       // all samples: ρ ~ 1e-4 at cfg5) sweeps from the warm start x = h_j reach the fp64 fixed
-      // point in a few steps (bound: ρ^nsw <= 2^-55, and a sweep that changes no bit ends early) —
+      // point in a few steps (bound: ρ^nsw <= 2^-55; exactly nsw sweeps run) —
       // the same solve as the block PCR below at a fraction of its per-row cost.
       HS_MARK(0);
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
@@ -5278,7 +5278,11 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
        if (jac) {
         // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P); the neighbours
         // x[2l-2], x[2l-1] from lane l - 1 and x[2l+2], x[2l+3] from lane l + 1
-        for (int sw = 0; sw < nsw; ++sw) {
+        // exactly nsw sweeps, no per-sweep convergence ballot (round 5: the ballot's VALU -> SALU ->
+        // branch round trip stalled every sweep; at cfg5's ρ ≈ 7e-5 the rows ran nsw = 5 sweeps anyway,
+        // and a sweep at the fixed point changes no bit)
+        const int nsw_s = __builtin_amdgcn_readfirstlane(nsw);
+        for (int sw = 0; sw < nsw_s; ++sw) {
           const double p0 = dpp_wave_shr(xf[0]), p1 = dpp_wave_shr(xf[1]);
           const double n0 = dpp_wave_shl(xf[0]), n1 = dpp_wave_shl(xf[1]);
           double r0 = rb[0];
@@ -5293,14 +5297,12 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           r1 = fma(-re2[1], n1, r1);
           const double x0 = pas[0] ? r0 * rinv[0] : 0.0;  // (pas is false past F)
           const double x1 = pas[1] ? r1 * rinv[1] : 0.0;
-          const bool chg = (x0 != xf[0]) || (x1 != xf[1]);
           xf[0] = x0;
           xf[1] = x1;
           cbad = ((pas[0] ? r0 < 0.0 : r0 > 0.0) ? 1 : 0) | ((pas[1] ? r1 < 0.0 : r1 > 0.0) ? 2 : 0);
 #ifdef CNMF_STAMPS
           hs_ph[1] += 1000ull;  // the stamps' "gather" slot counts the Jacobi sweeps (in thousands)
 #endif
-          if (!__ballot(chg)) break;
         }
         HS_MARK(2);
        } else {

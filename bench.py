@@ -68,9 +68,11 @@ def parse(argv=None):
                    help="weak (default): every GPU owns --rows rows, value = ranks x iterations/s in "
                         "'<rows>-row it/s'; strong: --rows is ONE problem split over the GPUs, value = "
                         "iterations/s of that problem")
-    p.add_argument("--strong-rows", type=int, default=1_000_000,
+    p.add_argument("--strong-rows", type=int, default=None,
                    help="at N > 1: also time this V (x F) as ONE problem split over the ranks, and on "
-                        "rank 0's GPU alone (the line's `strong` key); 0 = skip")
+                        "rank 0's GPU alone (the line's `strong` key); 0 = skip; default 1e6 (the "
+                        "metric's V), skipped when ranks share a GPU (their 1e6-row persistent grids "
+                        "are not co-resident on one device; ADVICE r5)")
     p.add_argument("--features", type=int, default=81)
     p.add_argument("--k", type=int, default=4)
     p.add_argument("--dtype", default="f32", choices=["f32", "f64", "bf16"])
@@ -672,6 +674,15 @@ def main():
     # the same ranks, and on rank 0's GPU alone (ranks > 0 wait at the barrier meanwhile)
     strong = None
     S = args.strong_rows
+    # ranks that share a device (--backend gloo on fewer GPUs): the default 1e6-row split is not
+    # co-resident there, so it is recorded as not measured unless --strong-rows asks for it
+    n_gpus = min(world, n_dev) if args.backend == "gloo" and dist_path else world
+    strong_skipped = None
+    if S is None:
+        S = 1_000_000
+        if world > 1 and n_gpus < world:
+            S, strong_skipped = 0, (f"not measured: {world} ranks share {n_gpus} GPU(s) (pass --strong-rows "
+                                    f"to split a problem whose per-rank grids are co-resident)")
     if world > 1 and S > 0:
         if args.scaling == "strong" and S == args.rows:
             sres, s_rows, s_plan = res, n_rows, None
@@ -699,6 +710,8 @@ def main():
             refuse_result("one-GPU reference of the strong split: " + (n1["problem"] if n1_bad else "rank 0"), rank)
         if rank == 0:
             strong = strong_block(args, sres, s_rows_max, S, world, n1)
+    elif strong_skipped:
+        strong = {"skipped": strong_skipped}
     elif world == 1 and S > 0 and n_rows == S and not args.dist:
         strong = strong_block(args, res, n_rows, S, 1)
         strong["n1_it_s"], strong["n1_us_per_iteration"], strong["speedup_vs_n1"] = (
@@ -794,8 +807,7 @@ def main():
                         f"{n_rows} rows of one {world * n_rows}-row problem, [WᵀX | WᵀW] all-reduced "
                         f"every iteration; value = {world} x the it/s of that problem = iterations of "
                         f"one {n_rows}-row shard per second over all ranks)")
-    # ranks that share a device (--backend gloo on fewer GPUs) are not more GPUs
-    n_gpus = min(world, n_dev) if args.backend == "gloo" and dist_path else world
+    # ranks that share a device (--backend gloo on fewer GPUs) are not more GPUs: n_gpus above
     out = {
         "metric": metric,
         "value": round(value, 2),

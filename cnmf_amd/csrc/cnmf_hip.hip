@@ -4882,14 +4882,18 @@ __global__ __launch_bounds__(256) void scale_columns_kernel(TC* __restrict__ W, 
 //     pivoting, scattered to 4x4 (zeros outside P), and a valid flag (pivot > 1e-13·max diag).
 // ------------------------------------------------------------------------------------------------
 constexpr int ALS_MAX_F = 512;
+// components of the constrained ALS: the W-step's passive-set table (16 masks), the one-wave H-step's
+// running right-hand-side update and its sweep-count slots are sized for it; every ALS entry point
+// refuses k > ALS_MAX_K with CNMF_ERR_UNSUPPORTED before any launch
+constexpr int ALS_MAX_K = 4;
 
 __host__ __device__ inline size_t als_pre_offset(int F, int k) {  // 16-B aligned, after the ints
   return (((size_t)2 * k * F + k * k + 9 * (size_t)F) * 8 + (3 * (size_t)F + 16) * 4 + 15) / 16 * 16;
 }
 __host__ __device__ inline size_t als_lds_bytes(int F, int k) {
   // doubles: A, H [k][F]; B [k][k]; b, x, d0, e1, e2, L0, L1, L2, z [F]; then ints: pas, inf, idx [F], 8;
-  // then (the one-wave form's per-row constants, round 5) bpre, rinv [k][F] and k sweep counts
-  return als_pre_offset(F, k) + ((size_t)2 * k * F + 4) * 8;
+  // then (the one-wave form's per-row constants, round 5) bpre, rinv [k][F] and ALS_MAX_K sweep counts
+  return als_pre_offset(F, k) + ((size_t)2 * k * F + ALS_MAX_K) * 8;
 }
 
 // M(fa, fb) of the row Hessian for |fa - fb| <= 2 (0 otherwise), fb < fa
@@ -5208,8 +5212,10 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
     const double* nswp = rinvp + (size_t)k * F;
     for (int j = 0; j < k; ++j) {
       // the row's operands in one batch of LDS reads.  bpre[j] already holds a_j − Σ_{m>j} B_jm·h_m(old)
-      // − Σ_{m<j} B_jm·h_m(new): each earlier row subtracted its new values at its end (below), in
-      // ascending m — the same operations in the same order as summing them here, so the same bits
+      // − Σ_{m<j} B_jm·h_m(new): the precompute subtracted the later rows (ascending m > j), each
+      // earlier row its new values at its end (below, ascending m < j) — a different rounding order
+      // from one sum over m != j for j >= 1 (the H-step agrees with scipy's sweep to ~1e-12 either
+      // way, tests/test_gpu_als.py::test_h_step_matches_scipy_nnls at 1e-9)
       const double bjj = sB[j * k + j];
       const int nsw = (int)nswp[j];
       double hjv[2], bv[2], riv[2];
@@ -5271,10 +5277,6 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // the same solve as the block PCR below at a fraction of its per-row cost.
       HS_MARK(0);
       for (int iter = 0; iter < 5 * F + 10; ++iter) {
-       // Jacobi: the KKT check from the last sweep's residuals r = b − (M − diag)·x (the sweep that
-       // changed no bit evaluates them at the final x): on P, x = r / M_ff < 0 iff r < 0; off P
-       // (x_f = 0) the dual y_f = (M x − b)_f = −r_f (past F, r = 0)
-       int cbad = 0;
        if (jac) {
         // ---- M_PP x = b_P by Jacobi sweeps over the row's features (x = 0 off P); the neighbours
         // x[2l-2], x[2l-1] from lane l - 1 and x[2l+2], x[2l+3] from lane l + 1
@@ -5299,7 +5301,6 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
           const double x1 = pas[1] ? r1 * rinv[1] : 0.0;
           xf[0] = x0;
           xf[1] = x1;
-          cbad = ((pas[0] ? r0 < 0.0 : r0 > 0.0) ? 1 : 0) | ((pas[1] ? r1 < 0.0 : r1 > 0.0) ? 2 : 0);
 #ifdef CNMF_STAMPS
           hs_ph[1] += 1000ull;  // the stamps' "gather" slot counts the Jacobi sweeps (in thousands)
 #endif
@@ -5395,12 +5396,11 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
         lds_order();
        }
         // the KKT check: x >= 0 on P, the dual y = (M x − b)_f >= 0 off P (neighbours outside the
-        // row enter with zero coefficients)
+        // row enter with zero coefficients), both from the x the sweep returns (the last
+        // Jacobi sweep's residuals use the neighbours before that sweep's update — exact only once it
+        // changed no bit; a cold start or a BPP flip far from the solution could misread a dual near 0)
         bool bad[2];
-        if (jac) {
-#pragma unroll
-          for (int c = 0; c < 2; ++c) bad[c] = (cbad >> c) & 1;
-        } else {
+        {
           const double p0 = dpp_wave_shr(xf[0]), p1 = dpp_wave_shr(xf[1]);
           const double n0 = dpp_wave_shl(xf[0]), n1 = dpp_wave_shl(xf[1]);
           const double nm1[2] = {p1, xf[0]}, np1[2] = {xf[1], n0}, nm2[2] = {p0, p1}, np2[2] = {n0, n1};
@@ -5456,7 +5456,7 @@ __device__ __forceinline__ void als_hstep_wave(unsigned char* smem, int F, int k
       // the later rows' right-hand sides take this row's new values (each lane its own features:
       // the later read is the same lane's, in order)
 #pragma unroll
-      for (int m = 1; m < 4; ++m)
+      for (int m = 1; m < ALS_MAX_K; ++m)  // k <= ALS_MAX_K (every ALS entry point checks it)
         if (m > j && m < k) {
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
@@ -7900,7 +7900,7 @@ static int als_basis_launch(const double* AB, double* H64, double* Ht, double* H
   int st = check_update_args(H64, Ht, HHt, F, k);
   if (st) return st;
   if (!table || (do_update && !AB)) return set_err(CNMF_ERR_ARG, "null pointer argument");
-  if (k > 4) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= 4 (got %d)", k);
+  if (k > ALS_MAX_K) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= %d (got %d)", ALS_MAX_K, k);
   if (F > ALS_MAX_F) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports F <= %d", ALS_MAX_F);
   if (!(lam >= 0.0) || !(delta >= 0.0)) return set_err(CNMF_ERR_ARG, "smoothness and sum_to_one must be >= 0");
   const size_t lds = std::max(als_lds_bytes(F, k), update_lds_doubles(F, k, 4) * sizeof(double));
@@ -7931,7 +7931,7 @@ int cnmf_als_sample_pass(const void* X, int x_dtype, void* W, const double* Ht, 
                          int accumulate, void* stream) {
   if (n_rows < 0) return set_err(CNMF_ERR_SHAPE, "n_rows < 0");
   if (!X || !W || !Ht || !table || (accumulate && !partials)) return set_err(CNMF_ERR_ARG, "null pointer argument");
-  if (k > 4) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= 4 (got %d)", k);
+  if (k > ALS_MAX_K) return set_err(CNMF_ERR_UNSUPPORTED, "constrained ALS supports k <= %d (got %d)", ALS_MAX_K, k);
   if (!(sum_to_one >= 0.0)) return set_err(CNMF_ERR_ARG, "sum_to_one must be >= 0");
   if ((reinterpret_cast<uintptr_t>(X) & 15) || (reinterpret_cast<uintptr_t>(W) & 15))
     return set_err(CNMF_ERR_ALIGN, "X and W must be 16-byte aligned");
@@ -8149,15 +8149,15 @@ static int resolve_layout(int layout) {
 #ifdef CNMF_DIAG
   return (layout >= 1 && layout <= 6) ? layout : -1;
 #else
-  return (layout >= 4 && layout <= 6) ? layout : -1;
+  return (layout == 4 || layout == 6) ? layout : -1;
 #endif
 }
 #define RESOLVE_LAYOUT(var)                                                                                  \
   do {                                                                                                      \
     var = resolve_layout(var);                                                                              \
     if (var < 0)                                                                                            \
-      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 4 (wave tiles), 5 (k = 8 wave tiles on "   \
-                     "the matrix cores) or 6 (cfg4 persistent); 1-3 are in the diagnostic build only");   \
+      return set_err(CNMF_ERR_ARG, "layout must be 0 (default), 4 (wave tiles) or 6 (cfg4 persistent); "   \
+                     "1-3 and 5 (k = 8 wave tiles on the matrix cores) are in the diagnostic build only");  \
   } while (0)
 static PassFn persist_teams_fn(bool multi) {
 #ifndef CNMF_DIAG
@@ -8242,14 +8242,25 @@ static PassFn wt_fn_k(int pd, bool multi, bool tol) {
     return multi ? reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true, true>)
                  : reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false, true>);
   if (multi) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, true>);
+#ifdef CNMF_DIAG  // the prefetch-depth sweeps (CNMF_WT_PD): diagnostic build only
   if (KK == 4 && WRES && pd == 2) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 2, false>);
   if (KK == 4 && WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<4, true, 4, false>);
   if (KK == 8 && !WRES && pd == 4) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<8, false, 4, false>);
   if (KK == 8 && !WRES && pd == 5) return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<8, false, 5, false>);
+#else
+  (void)pd;
+#endif
   return reinterpret_cast<PassFn>(&mu_iter_wt_kernel<KK, WRES, 3, false>);
 }
 }
+// the k = 8 matrix-core wave tiles (layout 5): slower than the VALU wave tiles on every box measured
+// (DESIGN §3.0), so since round 6 they exist in the diagnostic build only; the
+// product refuses layout 5 with CNMF_ERR_ARG
 static PassFn mf8_fn(bool wres, bool multi, bool tol) {
+#ifndef CNMF_DIAG
+  (void)wres; (void)multi; (void)tol;
+  return nullptr;
+#else
   if (wres)
     return tol ? (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, true, true>)
                         : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<true, 3, false, true>))
@@ -8259,6 +8270,7 @@ static PassFn mf8_fn(bool wres, bool multi, bool tol) {
                       : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, true>))
              : (multi ? reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, true, false>)
                       : reinterpret_cast<PassFn>(&mu_iter_mf8_kernel<false, 3, false, false>));
+#endif
 }
 static PassFn wt_fn(int k, bool wres, bool multi, bool tol = false) {
   const int pd = tol ? 3 : wt_pd(k, wres, multi);

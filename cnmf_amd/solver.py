@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -25,6 +26,15 @@ from ._lib import check
 from ._trace import trace_range
 
 _XDT = {torch.float32: _lib.F32, torch.float64: _lib.F64, torch.bfloat16: _lib.BF16}
+
+
+# Fault injection for the multi-GPU tests (SURVEY §5 "failure detection"; never set in a measured
+# run): CNMF_FAULT_XCHG_SETUP=1 makes THIS rank report its in-launch exchange setup as failed, so
+# every rank must agree to take the RCCL path; CNMF_FAULT_XCHG_POISON=1 sets this rank's error word
+# before its first exchange launch, so its top combiner tags its words XPOISON and every peer's
+# launch fails in the same iteration (tests/test_gpu_bench_dist.py).
+def _fault(name: str) -> bool:
+    return os.environ.get(name, "0") == "1"
 
 
 def _ptr(t: torch.Tensor | None):
@@ -138,9 +148,8 @@ class MUPlan:
         self.exchange_shape = self.persistent_shape and int(xg) > 0
         # the persistent layouts tune() chooses between for this shape (include/cnmf_hip.h `layout`):
         # cfg4's bf16 shape: the per-iteration launches (4) or ONE persistent launch (6).  k = 8 fp32
-        # takes the VALU wave tiles (4); the matrix-core tiles (5) stay selectable with set_layout(5)
-        # but are no longer timed on every run: they lost on every box measured (cfg3 shard 150.6 vs
-        # 110.7 us, profiles/r05/)
+        # takes the VALU wave tiles (4); the matrix-core tiles (5) lost on every box measured (cfg3
+        # shard 150.6 vs 110.7 us, profiles/r05/) and live in the diagnostic library only (round 6)
         self.layouts = ()
         if self.xdt == _lib.BF16 and self.world == 1 and not self.persistent_shape:
             with torch.cuda.device(self.device):
@@ -180,6 +189,8 @@ class MUPlan:
             if r != rank and j is not None and j != self.device.index and \
                     self.lib.cnmf_device_can_access_peer(self.device.index, j) != 1:
                 ok[0], err = 0.0, f"no peer access from device {self.device.index} to {j} ({bus})"
+        if _fault("CNMF_FAULT_XCHG_SETUP"):
+            ok[0], err = 0.0, "fault injected (CNMF_FAULT_XCHG_SETUP)"
         if self.exchange_shape and ok[0] != 0.0:
             hb = int(self.lib.cnmf_xbuf_handle_bytes())
             hbuf = ctypes.create_string_buffer(hb)
@@ -268,6 +279,13 @@ class MUPlan:
         buf = ctypes.create_string_buffer(64)
         check(self.lib.cnmf_device_pci_bus_id(dev, buf, 64), "cnmf_device_pci_bus_id")
         return buf.value.decode().lower()
+
+    def _inject_poison(self):
+        """CNMF_FAULT_XCHG_POISON=1 (tests only): this rank's error word set before its first exchange
+        launch — the launch's top combiner then tags its exchange words XPOISON (xchg_allreduce_n)."""
+        if _fault("CNMF_FAULT_XCHG_POISON") and not getattr(self, "_poisoned", False):
+            self._poisoned = True
+            self.counter[self.err_word] = 1
 
     def disable_exchange(self):
         """Back to shard steps + RCCL (the buffers stay mapped until the plan is released)."""
@@ -412,6 +430,7 @@ class MUPlan:
                 self.sample_pass(_lib.PASS_UPDATE_W)
             return
         if getattr(self, "exchange", False):
+            self._inject_poison()
             with torch.cuda.device(self.device):
                 check(self.lib.cnmf_mu_iterations_multi(
                     n_iter, _ptr(self.X), self.xdt, _ptr(self.W), _ptr(self.H64), _ptr(self.Ht),

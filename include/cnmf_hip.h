@@ -111,14 +111,13 @@ int cnmf_mu_persistent(int64_t n_rows, int n_features, int k, int x_dtype);
  *   0 = default (4);
  *   4 = wave tiles: one 4-wave workgroup per CU, each wave streaming its own 16-sample (k = 4) or
  *       8-sample (k = 8) tiles with no barrier inside an iteration, W resident in LDS when it fits;
- *   5 = k = 8 only: the wave tiles with both products on the matrix cores (v_mfma_f32_16x16x4_f32,
- *       16-sample tiles; n_rows a multiple of 16, else layout 4);
  *   6 = bf16 X, F = 289..320, k = 16, n_rows a multiple of 64 (cfg4): n iterations as ONE launch of
  *       mu_iter_bfw_kernel (the pass, the reduction and the basis update in the launch; one GPU);
  *       layout 4 is that shape's per-iteration launches;
- * MUPlan.tune() times 4 and 5 at k = 8 (4 and 6 for cfg4's shape) and keeps the faster for its
- * plan; other values are CNMF_ERR_ARG.  (Layouts 1-3, the round-1 workgroup-tile kernel, exist in the diagnostic build
- * only: DESIGN §3.0b.) */
+ * MUPlan.tune() times 4 and 6 for cfg4's shape and keeps the faster for its plan; other values are
+ * CNMF_ERR_ARG.  (Diagnostic build only: layouts 1-3, the round-1 workgroup-tile kernel, DESIGN
+ * §3.0b; and 5, k = 8 wave tiles with both products on the matrix cores, v_mfma_f32_16x16x4_f32 —
+ * slower than layout 4 on every box measured) */
 
 /* n_iter single-GPU MU iterations with no host synchronisation: the body of SK:831-870 for tol == 0
  * stretches.  Persistent shapes: one cooperative launch that also runs the cross-block reduction

@@ -208,6 +208,63 @@ def test_cfg5_full_size_steps_match_oracle():
     assert rel_fro(plan.H64.cpu().numpy(), Hr) < 1e-9
 
 
+def _masks(W):
+    """Passive set of every sample as a k-bit mask (bit j: w_j > 0)."""
+    return ((W > 0) * (1 << np.arange(W.shape[1]))).sum(1)
+
+
+@pytest.mark.timeout(900)
+def test_cfg5_full_size_persistent_kernel_matches_oracle():
+    """the kernel the cfg5 bench times — als_iter_wt_kernel<…, MX> with the KKT
+    warm start and the one-wave Jacobi H-step, as ONE persistent launch at 1e6 x 81, k = 4, delta = 1,
+    lambda = 0.5 — against oracle/als_ref.als_fit (passive-set enumeration W-step, scipy NNLS H-step)
+    over the same iterations, W and H at 1e-5.
+
+    Leg 1: 10 iterations from cfg5's own start (random W0: every sample's previous set is {0..3}, so
+    most tiles fail the KKT certificate and take the enumeration first, then the warm start holds).
+    Leg 2: from the launch's state with H perturbed by up to +-25 % per entry (fp64 on both sides),
+    8 more iterations: the perturbation moves the optimum of a large share of the samples to another
+    passive set, so the warm start's certificate fails there and holds elsewhere — both W-step paths
+    run in the same launch; the test checks that both kinds of sample occur."""
+    import torch
+    from cnmf_amd.solver import ALSPlan
+    from cnmf_amd.synthetic import iop_spectra, random_init
+    X = iop_spectra(1_000_000, 81, seed=0, dtype=np.float32)
+    W0, H0 = random_init(X, 4, 42)
+    Xd = X.astype(np.float64)
+    plan = ALSPlan(torch.from_numpy(X).cuda(), 4, sum_to_one=1.0, smoothness=0.5)
+    assert plan.persistent and "MX" in plan.describe()
+    plan.set_W(torch.from_numpy(W0))
+    plan.set_H(torch.from_numpy(H0))
+    plan.iterate(10)
+    plan.check_sync_error()
+    W1, H1 = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr, Hr, _ = als_ref.als_fit(Xd, W0.astype(np.float64), H0.astype(np.float64), max_iter=10, tol=0.0,
+                                sum_to_one=1.0, smoothness=0.5, w_step="enumerate")
+    e1 = (rel_fro(W1, Wr), rel_fro(H1, Hr))
+    print(f"leg 1 (10 iterations from cfg5's start): rel W {e1[0]:.2e} H {e1[1]:.2e}")
+    assert e1[0] <= 1e-5 and e1[1] <= 1e-5, e1
+    assert plan.counters_at_rest()
+
+    rng = np.random.default_rng(5)
+    Hp = H1 * (1.0 + 0.25 * rng.uniform(-1.0, 1.0, H1.shape))
+    plan.set_H(torch.from_numpy(Hp))  # W stays the launch's: the warm start reads its passive sets
+    plan.iterate(8)
+    plan.check_sync_error()
+    W2, H2 = plan.W.cpu().numpy(), plan.H64.cpu().numpy()
+    Wr2, Hr2, _ = als_ref.als_fit(Xd, W1.astype(np.float64), Hp, max_iter=8, tol=0.0, sum_to_one=1.0,
+                                  smoothness=0.5, w_step="enumerate")
+    e2 = (rel_fro(W2, Wr2), rel_fro(H2, Hr2))
+    # the first W-step after the perturbation: which samples' passive sets moved
+    Wf = als_ref.fcls_w_enumerate(Xd, Hp, 1.0)
+    moved = float(np.mean(_masks(Wf) != _masks(W1)))
+    print(f"leg 2 (perturbed H, 8 iterations): rel W {e2[0]:.2e} H {e2[1]:.2e}; passive set moved "
+          f"for {100 * moved:.1f} % of the samples")
+    assert 0.01 < moved < 0.99, moved  # both the re-enumeration and the certified warm start occur
+    assert e2[0] <= 1e-5 and e2[1] <= 1e-5, e2
+    assert (W2 >= 0).all() and (H2 >= 0).all()
+
+
 # ---- the persistent constrained-ALS launch (als_iter_wt_kernel: fp32, F = 81, k = 4, rows % 16 == 0)
 
 @pytest.mark.parametrize("delta, lam", [(0.0, 0.0), (1.0, 0.5), (3.0, 5.0)])

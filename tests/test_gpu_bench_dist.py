@@ -26,16 +26,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_two_ranks(extra, timeout=240):
+def _run_two_ranks(extra, timeout=240, rank_env=None):
+    """bench.py's two ranks on cuda:0; rank_env: {rank: {VAR: value}} added to that rank's environment
+    (the fault-injection switches of cnmf_amd/solver.py).  Without --strong-rows the bench records the
+    default 1e6-row split as not measured (ranks sharing a GPU)."""
     port = _free_port()
     procs = []
     for rank in range(2):
         env = dict(os.environ, RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE="2",
                    LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update((rank_env or {}).get(rank, {}))
         cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
                "--steps", "20", "--warmup", "20", "--no-cpu", "--ramp-seconds", "0.2", "--scaling", "strong"] + extra
-        if "--strong-rows" not in extra:  # the 1e6-row strong split's grids are not co-resident on one GPU
-            cmd += ["--strong-rows", "0"]
         procs.append(subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
@@ -65,6 +67,49 @@ def test_bench_two_ranks_one_gpu_exchange():
     assert len(lay) == 2 and lay[0] == lay[1]
     assert cfg["clock_ramp_trips"] >= 1
     assert res["roofline"]["iterations_per_launch"] == 20  # the 20 steps as ONE launch per rank
+    # the default 1e6-row strong split is not co-resident when ranks share a GPU
+    assert res["strong"] == {"skipped": res["strong"]["skipped"]} and "not measured" in res["strong"]["skipped"]
+
+
+@pytest.mark.timeout(300)
+def test_bench_exchange_setup_fault_moves_every_rank_to_rccl():
+    """one rank's exchange setup fails (CNMF_FAULT_XCHG_SETUP on rank 1 only):
+    enable_exchange agrees collectively, so BOTH ranks time the shard-step + collective path and the
+    line's config.exchange names the failing rank."""
+    res, outs = _run_two_ranks(["--rows", "32768"], rank_env={1: {"CNMF_FAULT_XCHG_SETUP": "1"}})
+    cfg = res["config"]
+    assert cfg["exchange"].startswith("unavailable") and "rank 1: fault injected" in cfg["exchange"], cfg["exchange"]
+    assert "RCCL path timed" in cfg["exchange"]
+    assert res["roofline"]["launches_timed"] == 20 and res["value"] > 0  # one shard step per iteration
+    assert "in-launch over xGMI" not in cfg["parallelism"]
+    for _, _, err in outs:  # both ranks reported the same decision
+        assert "in-launch exchange (16384 rows): unavailable" in err
+
+
+@pytest.mark.timeout(300)
+def test_bench_exchange_poisoned_launch_moves_every_rank_to_rccl():
+    """One rank's launch fails inside the exchange (CNMF_FAULT_XCHG_POISON on rank 1: its error word
+    set before its first exchange launch, so its top combiner tags its words XPOISON): the peer's
+    launch must fail in the same iteration (no 2 s timeout per iteration), validation fails on both
+    ranks together and both time the collective path; the results stay a valid factorisation."""
+    res, outs = _run_two_ranks(["--rows", "32768"], rank_env={1: {"CNMF_FAULT_XCHG_POISON": "1"}})
+    cfg = res["config"]
+    assert cfg["exchange"].startswith("failed validation"), cfg["exchange"]
+    assert res["roofline"]["launches_timed"] == 20 and res["value"] > 0
+    assert res["final_frobenius_error"] > 0
+    for _, _, err in outs:
+        assert "in-launch exchange (16384 rows): failed validation" in err
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_weighted_with_strong_split():
+    """--weighted at N = 2 through the whole bench, the strong split included (its plan is
+    released after the measurement): one line, the exchange validated for the weighted launch."""
+    res, outs = _run_two_ranks(["--rows", "16384", "--scaling", "weak", "--weighted", "--strong-rows", "32768"])
+    assert res["ranks"] == 2 and res["value"] > 0
+    assert res["config"]["exchange"].startswith("validated"), res["config"]["exchange"]
+    assert res["strong"]["rows"] == 32768 and res["strong"]["speedup_vs_n1"] > 0
+    assert "weighted" in res["metric"]
 
 
 @pytest.mark.timeout(300)

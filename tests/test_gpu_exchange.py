@@ -176,3 +176,89 @@ def test_self_exchange_k8(N):
         plan.release()
     finally:
         dist.destroy_process_group()
+
+
+def _wide_rank_main(rank, world, port, rows, q):
+    """One rank of the world-4 / world-8 exchange test: 12 + 18 iterations as two launches, then a
+    second plan (fresh buffers) running the 30 as one launch."""
+    try:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                                world_size=world)
+        X, W0, H0 = _data(world * rows, 7)
+        lo, hi = rank * rows, (rank + 1) * rows
+        outs = []
+        for split in ((12, 18), (30,)):
+            plan = _plan(X[lo:hi].copy(), W0[lo:hi].copy(), H0, group=dist.group.WORLD)
+            g = int(plan.lib.cnmf_persist_workgroups(plan.n_rows, 81, 4, 0, 0, 1))
+            plan.enable_exchange()
+            for n in split:
+                plan.iterate(n)
+            plan.check_sync_error()
+            torch.cuda.synchronize()
+            outs.append((plan.W.cpu().numpy(), plan.H64.cpu().numpy(), int(plan.xctl[3].item())))
+            assert plan.counters_at_rest()
+            dist.barrier()
+            plan.release()
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, outs, g, None))
+    except Exception as ex:  # reported to the parent
+        q.put((rank, None, None, f"{type(ex).__name__}: {ex}"))
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [4, 8])
+def test_wide_world_one_gpu_exchange(world):
+    """the in-launch exchange (cnmf_mu_iterations_multi) at world 4 and 8 before
+    the driver's 8-GPU node meets it — `world` processes on one GPU, each rank's grid capped by its
+    shard (4096 rows = 256 tiles = 16 workgroups per rank; 64-128 of the 256 CUs in all, so every
+    rank's persistent grid is co-resident) exchanging through IPC-mapped buffers with the slot-per-rank
+    generation / parity protocol.  Every rank must hold the same H bit for bit; W / H agree with the
+    single-process run on the whole X to summation-order noise and with the fp64 oracle at 1e-5; two
+    launches (12 + 18) equal one (30) bit for bit on every rank, and the device-side generation base
+    advanced by 30 on every rank."""
+    import torch
+    rows = 4096
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_wide_rank_main, args=(r, world, port, rows, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, outs, g, err = q.get(timeout=500)
+            out[r] = (outs, g, err)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    errs = [v[2] for v in out.values() if v[2]]
+    assert not errs, errs
+    assert sorted(out) == list(range(world))
+    grids = [out[r][1] for r in range(world)]
+    assert sum(grids) <= 256 and min(grids) >= 1, grids
+    H = out[0][0][0][1]
+    for r in range(world):
+        (Wa, Ha, gena), (Wb, Hb, genb) = out[r][0]
+        np.testing.assert_array_equal(Ha, H)  # rank-ordered sums: the same H on every rank
+        np.testing.assert_array_equal(Hb, Ha)  # split launches == one launch, bit for bit
+        np.testing.assert_array_equal(Wb, Wa)
+        assert gena == genb == 30
+    W = np.concatenate([out[r][0][0][0] for r in range(world)])
+    X, W0, H0 = _data(world * rows, 7)
+    ref = _plan(X, W0, H0)
+    ref.iterate(30)
+    ref.check_sync_error()
+    torch.cuda.synchronize()
+    assert rel_fro(H, ref.H64.cpu().numpy()) < 1e-6
+    assert rel_fro(W, ref.W.cpu().numpy()) < 1e-6
+    Wr, Hr, _ = mu_ref.mu_fit(X.astype(np.float64), W0.astype(np.float64), H0.astype(np.float64),
+                              max_iter=30, tol=0.0)
+    print(f"world {world}: grids {grids}; vs oracle W {rel_fro(W, Wr):.2e} H {rel_fro(H, Hr):.2e}")
+    assert rel_fro(W, Wr) <= 1e-5 and rel_fro(H, Hr) <= 1e-5

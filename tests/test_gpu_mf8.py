@@ -2,7 +2,15 @@
 whose two products run on v_mfma_f32_16x16x4_f32 (layout 5) against the fp64
 oracle (north-star bar 1e-5), against the VALU wave tiles (layout 4, the default: fp32 summation-order
 agreement), bit-for-bit repeatable across split launches, W resident (LDS) and streamed, with the
-regularised update."""
+regularised update.
+
+Since round 6 layout 5 lives in the diagnostic library only (it lost to layout 4
+on every box), so each case runs in a child process with CNMF_HIP_LIB = cnmf_amd/libcnmf_hip_diag.so
+(one process per case, sequential: the library is chosen when the process first loads it)."""
+import os
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -10,6 +18,33 @@ from golden_io import rel_fro
 from oracle import mu_ref
 
 pytestmark = pytest.mark.gpu
+
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_DIAG = os.path.join(_ROOT, "cnmf_amd", "libcnmf_hip_diag.so")
+
+
+def _in_diag(call: str):
+    """Run `call` (an expression over this module, imported as m) in a child on the diagnostic library."""
+    code = (f"import sys; sys.path[:0] = [{_ROOT!r}, {os.path.join(_ROOT, 'tests')!r}]; "
+            f"import test_gpu_mf8 as m; {call}")
+    r = subprocess.run([sys.executable, "-u", "-c", code], cwd=_ROOT, capture_output=True, text=True,
+                       timeout=500, env=dict(os.environ, CNMF_HIP_LIB=_DIAG))
+    print(r.stdout[-2000:])
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+def test_product_library_refuses_layout_5():
+    """The product library has no matrix-core k = 8 tiles: layout 5 is CNMF_ERR_ARG there."""
+    import ctypes
+    import torch
+    from cnmf_amd import _lib
+    if "diag" in _lib.lib_path():
+        pytest.skip("CNMF_HIP_LIB points at the diagnostic library")
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(256)
+    assert torch.cuda.is_available()
+    assert lib.cnmf_persist_describe(1_250_000, 81, 8, _lib.F32, 5, buf, 256) < 0
+    assert b"diagnostic build" in lib.cnmf_last_error()
 
 
 def _plan(X, W0, H0, layout=5, **regs):
@@ -22,9 +57,14 @@ def _plan(X, W0, H0, layout=5, **regs):
     return plan
 
 
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("n,iters", [(16 * 4000, 200), (1_250_000, 30)])
 def test_mf8_matches_oracle_and_valu(n, iters):
     """64k rows: W resident in LDS; 1.25e6 rows (cfg3's shard): W streamed with X."""
+    _in_diag(f"m.case_matches_oracle_and_valu({n}, {iters})")
+
+
+def case_matches_oracle_and_valu(n, iters):
     import torch
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(n, 81, seed=n % 1009, dtype=np.float32)
@@ -51,7 +91,12 @@ def test_mf8_matches_oracle_and_valu(n, iters):
     assert torch.equal(a.W, c.W) and torch.equal(a.H64, c.H64)
 
 
+@pytest.mark.timeout(600)
 def test_mf8_500_iterations_and_regularised():
+    _in_diag("m.case_500_iterations_and_regularised()")
+
+
+def case_500_iterations_and_regularised():
     from cnmf_amd.synthetic import iop_spectra, random_init
     X = iop_spectra(16 * 3125, 81, seed=2, dtype=np.float32)
     W0, H0 = random_init(X, 8, 42)

@@ -11,14 +11,17 @@ exactly that (400 B of scratch, every load followed by a scratch store) and prod
 at 2.5x the time (profiles/r04/k8pd/).  The compiler does not report it, so the shipped code object
 is checked here, from the library file itself:
 
-    python tools/kcheck.py [cnmf_amd/libcnmf_hip.so]
+    python tools/kcheck.py [cnmf_amd/libcnmf_hip.so] [--arch gfx950] [--llvm DIR]
 
 Extracts the gfx950 code object (llvm-objcopy .hip_fatbin, clang-offload-bundler), disassembles it
 (llvm-objdump) and, per kernel whose name matches the wave-tile families, collects the AGPRs that
 are destinations of `global_load_dwordx4 a[..]` and lists every other instruction that reads or
 writes one of them (besides the `ds_write_b128` / `ds_write_b64` staging stores from them and
 `s_waitcnt`), plus any `vmcnt` immediate
-above the 6-bit field.  Exit status 1 on a finding.
+above the 6-bit field.  Exit status 1 on a finding; 2 when the check itself could not run (LLVM
+tools missing, no code object for the arch) — reported apart from findings.  The arch
+defaults to CNMF_OFFLOAD_ARCH (the build's) or gfx950; the LLVM tools are taken from --llvm, else
+next to the hipcc the build used (HIPCC / <rocm>/lib/llvm/bin), else /opt/rocm/lib/llvm/bin.
 """
 from __future__ import annotations
 
@@ -28,23 +31,47 @@ import subprocess
 import sys
 import tempfile
 
+import shutil
+
 LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def llvm_dir() -> str:
+    """The LLVM tools next to the hipcc the build uses (HIPCC, else the one on PATH), else LLVM."""
+    for hip in (os.environ.get("HIPCC"), shutil.which("hipcc")):
+        if hip and os.path.exists(hip):
+            root = os.path.dirname(os.path.dirname(os.path.realpath(hip)))
+            for d in (os.path.join(root, "lib", "llvm", "bin"), os.path.join(root, "llvm", "bin")):
+                if os.path.exists(os.path.join(d, "llvm-objdump")):
+                    return d
+    return LLVM
+
+
+class ToolError(RuntimeError):
+    """The check could not run (not a finding)."""
 FAMILIES = re.compile(r"(mu_iter_wt_kernel|mu_iter_mf8_kernel|wmu_iter_wt_kernel|als_iter_wt_kernel|"
                       r"mu_pass_bfw_kernel|mu_iter_bfw_kernel)")
 OK_OPS = ("global_load_dwordx4", "ds_write_b128", "ds_write_b64", "s_waitcnt")
 
 
-def disassemble(lib: str) -> str:
-    """The gfx950 code object of `lib`, disassembled."""
+def disassemble(lib: str, arch: str = "gfx950", llvm: str = LLVM) -> str:
+    """The `arch` code object of `lib`, disassembled; ToolError when a tool is missing or fails."""
+    def run(cmd, **kw):
+        if not os.path.exists(cmd[0]):
+            raise ToolError(f"{cmd[0]} not found (pass --llvm DIR)")
+        r = subprocess.run(cmd, capture_output=True, **kw)
+        if r.returncode != 0:
+            err = r.stderr if isinstance(r.stderr, str) else r.stderr.decode(errors="replace")
+            raise ToolError(f"{os.path.basename(cmd[0])} failed ({r.returncode}): {err.strip()[-500:]}")
+        return r
     with tempfile.TemporaryDirectory() as d:
         fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "dev.co")
-        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib, os.devnull],
-                       check=True, capture_output=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"],
-                       check=True, capture_output=True)
-        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
-                              capture_output=True, text=True).stdout
+        run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fat}", lib, os.devnull])
+        run([f"{llvm}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
+             f"--targets=hipv4-amdgcn-amd-amdhsa--{arch}", f"--output={co}"])
+        if not os.path.exists(co) or os.path.getsize(co) == 0:
+            raise ToolError(f"{lib} holds no {arch} code object")
+        return run([f"{llvm}/llvm-objdump", "-d", "--no-show-raw-insn", co], text=True).stdout
 
 
 def kernels(dis: str):
@@ -86,8 +113,13 @@ def check_kernel(body):
     return len(dst), bad, big
 
 
-def main(lib: str) -> int:
-    dis = disassemble(lib)
+def main(lib: str, arch: str | None = None, llvm: str | None = None) -> int:
+    arch = arch or os.environ.get("CNMF_OFFLOAD_ARCH", "gfx950")
+    try:
+        dis = disassemble(lib, arch, llvm or llvm_dir())
+    except ToolError as e:
+        print(f"kcheck: could not check {lib} ({arch}): {e}", file=sys.stderr)
+        return 2
     n_bad, n_k = 0, 0
     for name, body in kernels(dis):
         if not FAMILIES.search(name):
@@ -105,5 +137,11 @@ def main(lib: str) -> int:
 
 
 if __name__ == "__main__":
+    import argparse
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "cnmf_amd", "libcnmf_hip.so")))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib", nargs="?", default=os.path.join(root, "cnmf_amd", "libcnmf_hip.so"))
+    ap.add_argument("--arch", default=None)
+    ap.add_argument("--llvm", default=None)
+    a = ap.parse_args()
+    sys.exit(main(a.lib, a.arch, a.llvm))

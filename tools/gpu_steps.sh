@@ -20,6 +20,9 @@
 #   prof <tag> <bench.py args...>      rocprofv3 --kernel-trace --stats of a bench run -> <tag>/
 #   pmc <tag> "<counters>" <script args...>  one rocprofv3 --pmc pass over a python script -> <tag>/
 #   py <tag> <script args...>          python <script> -> <tag>.log
+#   benchenv <tag> <VAR=v> <lib> <bench.py args...>   bench on <lib> with one diagnostic switch set
+#   tlenv <tag> <VAR=v> <args...>      the timeline on the stamps build with one diagnostic switch set
+#   pytestenv <tag> <VAR=v> <lib> <pytest args...>     pytest on <lib> with one diagnostic switch set
 #   pylib <tag> <lib> <script args...> the same with CNMF_HIP_LIB=<lib>
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
@@ -65,6 +68,15 @@ for st in "$@"; do
       CNMF_HIP_LIB=$lib timeout -k 10 400 python -u "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
     py)
       timeout -k 10 400 python -u "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
+    benchenv)
+      kv=$1; lib=$2; shift 2
+      env "$kv" CNMF_HIP_LIB=$lib timeout -k 10 400 python -u bench.py "$@" > "$D/$tag.json" 2> "$D/$tag.err" || { tail -20 "$D/$tag.err"; exit 1; } ;;
+    tlenv)
+      kv=$1; shift
+      env "$kv" CNMF_HIP_LIB=cnmf_amd/libcnmf_hip_stamps.so timeout -k 10 300 python -u tools/timeline_persist.py "$@" > "$D/$tag.log" 2>&1 || { tail -20 "$D/$tag.log"; exit 1; } ;;
+    pytestenv)
+      kv=$1; lib=$2; shift 2
+      env "$kv" CNMF_HIP_LIB=$lib timeout -k 10 900 python -u -m pytest -x -q -p no:cacheprovider --timeout 300 --timeout-method thread "$@" > "$D/$tag.log" 2>&1 || { tail -30 "$D/$tag.log"; exit 1; } ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
 done

@@ -2165,8 +2165,12 @@ constexpr int DYN_MAX_POOLS = sl::GROUP * sl::MAX_GROUPS / DYN_GRP;
 constexpr int CNT_POOL = CNT_ERR + 32;           // floating-tile pools [parity][pool] (32-word stride)
 constexpr int CNT_RCOL0 = CNT_POOL + 2 * DYN_MAX_POOLS * 32;          // reduce_kernel: one ticket per 64-column block
 constexpr int CNT_UPD = CNT_POOL;  // basis_update_split_kernel's ticket (the pools serve layout 3 only)
+// the wave-tile kernels' XCC table (round 6): word b = 1 + the XCC id workgroup b runs on (written at
+// the launch's start, zeroed by the launch's last combiner), in the pools' words past CNT_UPD's line
+constexpr int CNT_XCC0 = CNT_POOL + 32;
 constexpr int RED_MAX_COLS = 512;
 constexpr int CNT_WORDS = CNT_RCOL0 + RED_MAX_COLS;
+static_assert(CNT_XCC0 + sl::GROUP * sl::MAX_GROUPS <= CNT_RCOL0, "the XCC table fits the pools' words");
 
 // sHt (fp32 [84][4], rows >= 81 zero) and sHHt (fp64 [4][4]) from the fp64 H in LDS; the HHᵀ
 // arithmetic (lanes over f, fixed shuffle tree) is that of basis_update_block.
@@ -2247,6 +2251,12 @@ struct PersistArgs {
   uint64_t* xctl;
   // TOL (the tolerance test on the device, SK:872-884): the control block of TC_* doubles
   double* tolctl;
+  // the wave-tile kernel's first reduction level through the XCD's L2 (round 6):
+  // a group's members (b ≡ g mod NG: one XCD under round-robin placement) store their partial rows
+  // with plain stores, kept in the L2 their combiner reads with sc1 loads — from the second iteration
+  // on, and only when the XCC table shows every member of the group on the combiner's XCC (placement
+  // is never assumed: a group spread over XCDs keeps the write-through stores)
+  int l2rows = 0;
 };
 
 // tolerance control block (doubles; TC_WSNAP holds a pointer's bits): inputs tol, it0 (global index
@@ -2318,8 +2328,15 @@ struct BfwArgs {
 // runtime bounds every K-step and feature block was its own basic block: phases 1 and 3 ran as
 // dependent chains, 2647 and 2263 cycles per wave tile, profiles/r03/bfw/); KSC = 0: runtime F, k.
 // PERSIST (KSC = 10, KC = 16 only): the n_iter iterations of mu_iter_bfw_kernel (below).
-template <int KSC, int KC, bool PERSIST>
+// NHT: H in NHT bf16 terms in phase 1.  Round 6 measured two terms (sixteen
+// significant bits of H: a third fewer phase-1 MFMAs and H reads) and kept three: cfg4 1.7-4 %
+// faster per iteration, but the dropped term's bias (the same rounding of H for every sample) moved
+// W 5x further from the fp64 oracle — 2.3e-6 against 4.7e-7 after 40 iterations, 5.1e-6 against
+// 1.9e-6 after cfg4's 500 (profiles/r06/cfg4_hterms/) — half the 1e-5 bar for 2-4 % of speed.
+// CNMF_BFW_HTERMS=2 selects it in the diagnostic build.
+template <int KSC, int KC, bool PERSIST, int NHT = 3>
 __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
+  static_assert(NHT == 2 || NHT == 3, "H in two or three bf16 terms in phase 1");
   using namespace bw;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const bf16_t* __restrict__ X = a.X;
@@ -2459,10 +2476,12 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
       const s16x8 c = *reinterpret_cast<const s16x8*>(xa1 + 64 * ks);
       const bf16x8 b1 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 64 * ks));
       const bf16x8 b2 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + bm::KP * L.hrow + 64 * ks));
-      const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
       const bf16x8 av = __builtin_bit_cast(bf16x8, a), cv = __builtin_bit_cast(bf16x8, c);
-      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
-      v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
+      if constexpr (NHT == 3) {
+        const bf16x8 b3 = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(hb + 2 * bm::KP * L.hrow + 64 * ks));
+        u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b3, u, 0, 0, 0);
+        v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b3, v, 0, 0, 0);
+      }
       u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b2, u, 0, 0, 0);
       v = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cv, b2, v, 0, 0, 0);
       u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, b1, u, 0, 0, 0);
@@ -2846,7 +2865,7 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
   }
 }
 
-template <int KSC, int KC>
+template <int KSC, int KC, int NHT = 3>
 __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __restrict__ X, float* __restrict__ W,
                                                             const double* __restrict__ Ht,
                                                             const double* __restrict__ HHt,
@@ -2866,7 +2885,7 @@ __global__ __launch_bounds__(NT, 1) void mu_pass_bfw_kernel(const bf16_t* __rest
   a.l2 = l2;
   a.flags = flags;
   a.n_tiles = n_tiles;
-  bfw_run<KSC, KC, false>(a);
+  bfw_run<KSC, KC, false, NHT>(a);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2928,6 +2947,21 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
     if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl[((it_) * TL_WG + b) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define TL_PUB(it_) do { if (t == 0 && (it_) < TL_IT) g_tl_pub[it_] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// per-level stamps of the reduction tree (round 6): [it][g][0] group g's combiner's ticket returned,
+// [1] its group row stored (vmcnt(0) + barrier); [it][TL_LVG][0] the top's ticket returned, [1] AB summed
+// and stored; and [it][wg] each workgroup's time before its partial-row stores (g_tl_pre)
+constexpr int TL_LVG = 64;
+__device__ unsigned long long g_tl_lv[TL_IT * (TL_LVG + 1) * 2];
+__device__ unsigned long long g_tl_pre[TL_IT * TL_WG];
+__device__ unsigned long long g_tl_seen[TL_IT * TL_WG];  // flag seen (non-top workgroups)
+__device__ unsigned long long g_tl_ab[TL_IT * TL_WG];    // AB in LDS (non-top workgroups)
+#define TL_LV(it_, g_, slot_)                                                                   \
+  do {                                                                                          \
+    if (t == 0 && (it_) < TL_IT) g_tl_lv[((it_) * (TL_LVG + 1) + (g_)) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define TL_PRE(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_pre[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_SEEN(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_seen[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_AB(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_ab[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_X(it_, slot_) do { if (t == 0 && (it_) < TL_IT) g_tl_x[(it_) * 4 + (slot_)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_START                                                                               \
   do {                                                                                         \
@@ -2945,6 +2979,10 @@ __device__ unsigned int g_tl_hw[TL_WG * 2];  // HW_REG_HW_ID (cu / sh / se bits)
 #define TL_PUB(it_) do {} while (0)
 #define TL_X(it_, slot_) do {} while (0)
 #define TL_START do {} while (0)
+#define TL_LV(it_, g_, slot_) do {} while (0)
+#define TL_PRE(it_) do {} while (0)
+#define TL_SEEN(it_) do {} while (0)
+#define TL_AB(it_) do {} while (0)
 #endif
 
 // The cross-rank all-reduce of AB (k(F+k) fp64) inside a persistent launch, run by the top
@@ -3608,6 +3646,100 @@ __device__ __forceinline__ void sum_rows_n(const double* rows, int m0, int step,
     }
 }
 
+// 16-byte agent-scope (sc1) loads and stores: the valid-forms table's first row allows 16-B sc1
+// stores and loads on both sides of a hand-off (MI355X_MICROARCH.md); one instruction per two doubles
+// where sum_rows_n moved 8 bytes per lane (round 6: the guide's 8-B accesses run at 0.54-0.70x the
+// 16-B rate, and the tail's combines were latency-bound on those loads, profiles/r06/tree/)
+__device__ __forceinline__ void ld16_sc1(u32x4& r, const double* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+}
+__device__ __forceinline__ void st16_sc1v(double* p, double v0, double v1) {
+  const u32x4 v = u32x4{(unsigned)__double2loint(v0), (unsigned)__double2hiint(v0), (unsigned)__double2loint(v1),
+                        (unsigned)__double2hiint(v1)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st16_plain(double* p, double v0, double v1) {
+  const u32x4 v = u32x4{(unsigned)__double2loint(v0), (unsigned)__double2hiint(v0), (unsigned)__double2loint(v1),
+                        (unsigned)__double2hiint(v1)};
+  asm volatile("global_store_dwordx4 %0, %1, off" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ double lo_d(const u32x4& r) { return __hiloint2double((int)r[1], (int)r[0]); }
+__device__ __forceinline__ double hi_d(const u32x4& r) { return __hiloint2double((int)r[3], (int)r[2]); }
+template <int N>
+__device__ __forceinline__ void wait8(u32x4 (&x)[8]) {
+  asm volatile("s_waitcnt vmcnt(%8)"
+               : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7])
+               : "n"(N) : "memory");
+}
+// sum_rows_n for an even NOUT with 16-byte sc1 loads: thread t owns the chunks (doubles 2c, 2c + 1)
+// c = t (and c = t + NT when NOUT / 2 > NT: k = 8) of every row and adds the rows in row order
+// (0.0 + r0 + r1 + ...: the same operations, the same bits as sum_rows_n); 16 loads in flight per
+// batch (one chunk: 16 rows, two waits of 8 in issue order; two chunks: 8 rows each); the result
+// goes to lds_out (optional) and, with 16-byte sc1 stores, to g_out
+template <int NOUT>
+__device__ __forceinline__ void sum_rows_v(const double* rows, int m0, int step, int cnt, double* lds_out,
+                                           double* g_out, int t) {
+  static_assert(NOUT % 2 == 0 && NOUT / 2 <= 2 * NT, "one or two 16-byte chunks per thread");
+  constexpr int NCH = NOUT / 2, UC = NCH > NT ? 2 : 1;
+  const int c0 = t < NCH ? t : NCH - 1;                    // threads past the row re-load its last chunk
+  const int c1 = t + NT < NCH ? t + NT : NCH - 1;          // (never stored)
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+  if constexpr (UC == 1) {
+    for (int m = 0; m < cnt; m += 16) {
+      u32x4 xa[8], xb[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ld16_sc1(xa[r], rows + (size_t)(m0 + min(m + r, cnt - 1) * step) * NOUT + 2 * c0);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) ld16_sc1(xb[r], rows + (size_t)(m0 + min(m + 8 + r, cnt - 1) * step) * NOUT + 2 * c0);
+      wait8<8>(xa);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v0 += m + r < cnt ? lo_d(xa[r]) : 0.0;
+        v1 += m + r < cnt ? hi_d(xa[r]) : 0.0;
+      }
+      wait8<0>(xb);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v0 += m + 8 + r < cnt ? lo_d(xb[r]) : 0.0;
+        v1 += m + 8 + r < cnt ? hi_d(xb[r]) : 0.0;
+      }
+    }
+  } else {
+    for (int m = 0; m < cnt; m += 8) {
+      u32x4 xa[8], xb[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const size_t row = (size_t)(m0 + min(m + r, cnt - 1) * step) * NOUT;
+        ld16_sc1(xa[r], rows + row + 2 * c0);
+        ld16_sc1(xb[r], rows + row + 2 * c1);
+      }
+      wait8<0>(xa);  // (both arrays' loads are interleaved: wait for all)
+      wait8<0>(xb);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        v0 += m + r < cnt ? lo_d(xa[r]) : 0.0;
+        v1 += m + r < cnt ? hi_d(xa[r]) : 0.0;
+        v2 += m + r < cnt ? lo_d(xb[r]) : 0.0;
+        v3 += m + r < cnt ? hi_d(xb[r]) : 0.0;
+      }
+    }
+  }
+  if (t < NCH) {
+    if (lds_out) {
+      lds_out[2 * t] = v0;
+      lds_out[2 * t + 1] = v1;
+    }
+    st16_sc1v(g_out + 2 * t, v0, v1);
+  }
+  if (UC == 2 && t + NT < NCH) {
+    if (lds_out) {
+      lds_out[2 * (t + NT)] = v2;
+      lds_out[2 * (t + NT) + 1] = v3;
+    }
+    st16_sc1v(g_out + 2 * (t + NT), v2, v3);
+  }
+}
+
 // the cross-rank all-reduce of AB inside a persistent launch (xchg_allreduce_ab's protocol,
 // generic in the accumulator count NOUT; slot stride 2·NOUT words)
 template <int NOUT>
@@ -3698,10 +3830,98 @@ __device__ __forceinline__ void xchg_allreduce_n(uint64_t* xctl, double* AB, dou
   TL_X(it, 3);
 }
 
+// HHᵀ (fp64) from the fp64 H in LDS: NT / K² consecutive threads per entry (16 at k = 4: one DPP row;
+// 4 at k = 8: a quad), each a strided part of the F products, then a fixed DPP butterfly over the
+// group (xor 1, xor 2 by quad_perm; at 16 the half-row and row mirrors) — register moves where the
+// round-5 xor tree went through the LDS crossbar (ds_bpermute, a dependent round trip per level).
+// Every entry takes the same operations in the same order, and HHᵀ[j][m] / HHᵀ[m][j] are the same
+// products, so it stays exactly symmetric.  Caller synchronises.
+template <int KK, class G = wt::Geo<KK>>
+__device__ __forceinline__ void wt_hht(unsigned char* smem, int t) {
+  const double* sH = reinterpret_cast<const double*>(smem + G::L_H);
+  double* sHHt = reinterpret_cast<double*>(smem + G::L_HHT);
+  constexpr int NE = KK * KK, TPE = NT / NE;
+  static_assert(TPE * NE == NT && (TPE == 4 || TPE == 16), "threads per HHᵀ entry: a quad or a DPP row");
+  const int en = t / TPE, part = t - en * TPE;
+  const int j = en / KK, m = en - (en / KK) * KK;
+  double v = 0.0;
+  for (int f = part; f < wt::F; f += TPE) v = fma(sH[j * wt::F + f], sH[m * wt::F + f], v);
+  v += wt::dpp64<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += wt::dpp64<0x4E>(v);  // quad_perm [2,3,0,1]
+  if constexpr (TPE == 16) {
+    v += wt::dpp64<0x141>(v);  // row_half_mirror: the other quad of the half-row
+    v += wt::dpp64<0x140>(v);  // row_mirror: the other half-row
+  }
+  if (part == 0) sHHt[en] = v;
+}
+// Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) and HHᵀ from the fp64 H in LDS — sl_derive_basis
+// for k = KK
+template <int KK, class G = wt::Geo<KK>>
+__device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
+  const double* sH = reinterpret_cast<const double*>(smem + G::L_H);
+  float* sHt = reinterpret_cast<float*>(smem + G::L_HT);
+  for (int e = t; e < G::NL * G::NQ * KK; e += NT) {
+    const int f = e / KK;
+    const int j = e - f * KK;
+    sHt[e] = f < wt::F ? (float)sH[j * wt::F + f] : 0.f;
+  }
+  wt_hht<KK, G>(smem, t);
+  __syncthreads();
+}
+// H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728) —
+// sl_update_basis for k = KK.  Round 6: the quotient as div_nr (v_rcp_f64 + one Newton step, the
+// W-update's arithmetic) and the new Hᵀ written with the new H (its pad rows stay zero), then HHᵀ
+template <int KK, class G = wt::Geo<KK>>
+__device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, double l1, double l2) {
+  constexpr int KF = KK * wt::F;
+  constexpr int U = (KF + NT - 1) / NT;
+  double* sH = reinterpret_cast<double*>(smem + G::L_H);
+  float* sHt = reinterpret_cast<float*>(smem + G::L_HT);
+  const double* sAB = reinterpret_cast<const double*>(smem + G::L_AB);
+  double hn[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + NT * u;
+    hn[u] = 0.0;
+    if (e < KF) {
+      const int j = e / wt::F;
+      const int f = e - j * wt::F;
+      const double h = sH[e];
+      const double num = sAB[j * G::V + f];                                      // (WᵀX)[j][f], SK:639
+      double den = 0.0;                                                          // ((WᵀW)·H)[j][f], SK:640
+      for (int m = 0; m < KK; ++m) den = fma(sAB[j * G::V + wt::F + m], sH[m * wt::F + f], den);
+      if (l1 > 0.0) den += l1;                                                   // SK:702-703
+      if (l2 > 0.0) den = den + l2 * h;                                          // SK:704-705
+      if (den == 0.0) den = EPS32;                                               // SK:706
+      hn[u] = h * div_nr(num, den);                                              // SK:722-726
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = t + NT * u;
+    if (e < KF) {
+      const int j = e / wt::F;
+      const int f = e - j * wt::F;
+      sH[e] = hn[u];
+      sHt[f * KK + j] = (float)hn[u];
+    }
+  }
+  // Hᵀ's pad rows (features >= F, read by the lanes past F): zero (a launch that starts with the
+  // pending update, apply_first, has not run wt_derive_basis)
+  for (int e = wt::F * KK + t; e < G::NL * G::NQ * KK; e += NT) sHt[e] = 0.f;
+  __syncthreads();
+  wt_hht<KK, G>(smem, t);
+  __syncthreads();
+}
+
+// The round-5 forms of wt_derive_basis / wt_update_basis (xor-shuffle HHᵀ tree, IEEE division), kept
+// for k = 8: the round-6 end of iteration measured 3.5 % slower on cfg3's k = 8 shard (the streaming
+// body's schedule, not the tail; profiles/r06/tree/), so that kernel keeps the round-5 tail.
 // Hᵀ (fp32, the lanes' feature blocks, rows >= F zero) and HHᵀ (fp64; lanes over f, fixed shuffle
 // tree) from the fp64 H in LDS — sl_derive_basis for k = KK
 template <int KK, class G = wt::Geo<KK>>
-__device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
+__device__ __forceinline__ void wt_derive_basis_r5(unsigned char* smem, int t) {
   const double* sH = reinterpret_cast<const double*>(smem + G::L_H);
   float* sHt = reinterpret_cast<float*>(smem + G::L_HT);
   double* sHHt = reinterpret_cast<double*>(smem + G::L_HHT);
@@ -3727,7 +3947,7 @@ __device__ __forceinline__ void wt_derive_basis(unsigned char* smem, int t) {
 // H <- H·(WᵀX / ((WᵀW)·H (+l1)(+l2·H))) on the fp64 H in LDS from AB in LDS (SK:634-728) —
 // sl_update_basis for k = KK
 template <int KK, class G = wt::Geo<KK>>
-__device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, double l1, double l2) {
+__device__ __forceinline__ void wt_update_basis_r5(unsigned char* smem, int t, double l1, double l2) {
   constexpr int KF = KK * wt::F;
   constexpr int U = (KF + NT - 1) / NT;
   double* sH = reinterpret_cast<double*>(smem + G::L_H);
@@ -3755,7 +3975,7 @@ __device__ __forceinline__ void wt_update_basis(unsigned char* smem, int t, doub
   for (int u = 0; u < U; ++u)
     if (t + NT * u < KF) sH[t + NT * u] = hn[u];
   __syncthreads();
-  wt_derive_basis<KK, G>(smem, t);
+  wt_derive_basis_r5<KK, G>(smem, t);
 }
 
 // TOL: the tolerance test of SK:872-884 on the device.  In iteration g + 1 (g = it0 + it, g % 10 ==
@@ -3772,6 +3992,11 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   using G_ = Geo<KK>;
   constexpr int NL = G_::NL, TSW = G_::TSW, NQ = G_::NQ, V = G_::V, NOUT = G_::NOUT;
   constexpr int NOUTT = NOUT + (TOL ? 1 : 0);  // partial-row width: + the loss of the checked state
+  // row stride of the partial / group rows and AB: even, so that every row is 16-byte chunks (round 6:
+  // 16-byte sc1 hand-offs; TOL's odd NOUTT + a zero pad — cnmf_mu_fit_tol's rows of k(F+k) + 2)
+  // k = 8 keeps the round-5 tail (8-byte hand-offs, the round-5 basis update; see wt_update_basis_r5)
+  constexpr bool R6 = KK == 4;
+  constexpr int RS = R6 ? (NOUTT + 1) & ~1 : NOUTT;
   constexpr int XBW = G_::XBW, XSTR = G_::XSTR, WBW = G_::WBW, NACC = G_::NACC;
   constexpr int PFW = G_::PFW, LASTL = G_::LASTL;
   constexpr int PFS = PFW + (WRES ? 0 : 1);  // loads per prefetch set (+ the W tile when streamed)
@@ -3837,6 +4062,14 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   uint32_t* err = a.cnt + CNT_ERR;
 
   // ---- the basis for the first iteration, the staging pads, this wave's W tiles (W resident)
+  const bool l2rows = R6 && a.l2rows != 0;
+  if (t == 0) {  // the XCC this workgroup runs on, into the table (read once, after iteration 0)
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    sFlag[4] = 0;  // partial rows write-through until the group's placement has been checked
+    sFlag[5] = (int)(xcc & 0xFu) + 1;
+    if (l2rows) __hip_atomic_store(a.cnt + CNT_XCC0 + b, (xcc & 0xFu) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (int i = t; i < KK * F; i += NT) sH[i] = a.H64[i];
   if (a.apply_first)
     for (int i = t; i < NOUT; i += NT) sAB[i] = a.AB[i];
@@ -3850,10 +4083,13 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
   }
   __syncthreads();
-  if (a.apply_first)
-    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
-  else
-    wt_derive_basis<KK>(smem, t);
+  if (a.apply_first) {
+    if constexpr (R6) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+    else wt_update_basis_r5<KK>(smem, t, a.l1H, a.l2H);
+  } else {
+    if constexpr (R6) wt_derive_basis<KK>(smem, t);
+    else wt_derive_basis_r5<KK>(smem, t);
+  }
 
   // the lane's Hᵀ (fp32 component pairs of each of its NQ features) and HHᵀ row e
   f2 hp[NQ][KP];
@@ -3916,7 +4152,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
   // younger than it when its step waits (set q < PD: PD - q dummies, then the W stores of bodies
   // 0..q-1).  Counting PD stores that were never issued would let the set's last loads (the W tile)
   // still be in flight when it is staged.
-  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * NOUTT) + 64 * w + l;
+  float* dummy = reinterpret_cast<float*>(a.partials + (size_t)b * RS) + 64 * w + l;
 #pragma unroll
   for (int k = 0; k < PD; ++k) {
     prefetch(pf[k], gw + (int64_t)NW * k, k);  // the host keeps nbt > PD
@@ -4132,21 +4368,33 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       lossacc = 0.0;
     }
     __syncthreads();
+    TL_PRE(it);
     // the workgroup's fp64 row [K][V] (+ the loss): the four waves' sums in wave order (deterministic)
     {
-      double* prow = a.partials + (size_t)b * NOUTT;
-      if (TOL && t == 0)
-        __hip_atomic_store(prow + NOUT, (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      for (int o = t; o < NOUT; o += NT) {
+      double* prow = a.partials + (size_t)b * RS;
+      const bool plain = sFlag[4] != 0;  // the group's rows through the XCD's L2 (l2rows)
+      auto row_val = [&](int o) {
         const int j = o / V;
         const int v = o - j * V;
         const int ee = v < F ? v / NQ : j;
         const int idx = v < F ? (v - NQ * ee) * KK + j : NQ * KK + (v - F);
         const float* rr = red + ee * NACC + idx;
         constexpr int WS = NL * NACC;  // wave stride
-        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
-        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+      };
+      // pairs of doubles, one 16-byte store each (round 6); TOL: the loss at NOUT, a zero pad after it
+      auto val = [&](int o) {
+        if (o < NOUT) return row_val(o);
+        return (TOL && o == NOUT) ? (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]) : 0.0;
+      };
+      if constexpr (R6) {
+        for (int c = t; c < RS / 2; c += NT) {
+          const double v0 = val(2 * c), v1 = val(2 * c + 1);
+          if (plain) st16_plain(prow + 2 * c, v0, v1);
+          else st16_sc1v(prow + 2 * c, v0, v1);
+        }
+      } else {
+        for (int o = t; o < NOUTT; o += NT) __hip_atomic_store(prow + o, val(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
@@ -4164,19 +4412,29 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     // there must reach every workgroup before it writes W back)
     const bool must_wait = !last_it || loss_it;
     if (sFlag[0]) {  // group combiner
-      sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
+      TL_LV(it, g, 0);
+      if constexpr (R6) sum_rows_v<RS>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * RS, t);
+      else sum_rows_n<RS>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * RS, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      TL_LV(it, g, 1);
       if (t == 0) {
         const uint32_t old = __hip_atomic_fetch_add(cnt_top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sFlag[1] = old == (uint32_t)((it + 1) * NG - 1);
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
-        sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        TL_LV(it, TL_LVG, 0);
+        if constexpr (R6) {
+          sum_rows_v<RS>(a.groups, 0, 1, NG, sAB, a.AB, t);
+          if (MULTI) __syncthreads();  // the exchange reads sAB in sum_rows_n's thread mapping
+        } else {
+          sum_rows_n<RS>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        }
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        TL_LV(it, TL_LVG, 1);
         // (after the barrier: the summed loss sAB[NOUT] was written by another thread)
         if (TOL && loss_it && t == 0) {  // SK:872-884 on the state after it0 + it iterations
           const int gi = it0 + it;
@@ -4224,6 +4482,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
           __builtin_amdgcn_s_sleep(1);
         }
         if (TOL && (f & FLAG_STOP)) sFlag[3] = 1;
+        TL_SEEN(it);
       }
       __syncthreads();
       if (!sFlag[2]) {  // a workgroup never arrived (not co-resident): give up, error word set
@@ -4251,6 +4510,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (l2rows)
+        for (int o = t; o < G; o += NT) __hip_atomic_store(a.cnt + CNT_XCC0 + o, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         st_sc1(a.tolctl + TC_DONE, (double)(it0 + it));
@@ -4271,7 +4532,10 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
         }
       if (!top) return;
       // the last combiner of the launch: every other workgroup has arrived for the last time
-      if (a.apply_last) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+      if (a.apply_last) {
+        if constexpr (R6) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+        else wt_update_basis_r5<KK>(smem, t, a.l1H, a.l2H);
+      }
       for (int o = t; o < KK * F; o += NT) a.H64[o] = sH[o];
       for (int o = t; o < F * KK; o += NT) {
         const int f = o / KK;
@@ -4280,6 +4544,8 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       }
       if (t < KK * KK) a.HHt[t] = reinterpret_cast<const double*>(smem + G_::L_HHT)[t];
       if (t < NG) __hip_atomic_store(a.cnt + CNT_GROUP0 + 32 * t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (l2rows)
+        for (int o = t; o < G; o += NT) __hip_atomic_store(a.cnt + CNT_XCC0 + o, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
         __hip_atomic_store(cnt_top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!must_wait)  // (else workgroups may still poll it: the host clears it after the launch)
@@ -4294,15 +4560,43 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
       return;
     }
     if (!top) {
-      for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      if constexpr (!R6) {
+        for (int o = t; o < NOUTT; o += NT) sAB[o] = ld_sc1(a.AB + o);
+      } else {  // 16-byte sc1 loads, all in flight together (round 6)
+        constexpr int NCH = RS / 2;
+        const int c0 = t < NCH ? t : 0, c1 = t + NT < NCH ? t + NT : 0;
+        u32x4 r0, r1;
+        ld16_sc1(r0, a.AB + 2 * c0);
+        if (NCH > NT) ld16_sc1(r1, a.AB + 2 * c1);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(r0), "+v"(r1) : : "memory");
+        if (t < NCH) {
+          sAB[2 * t] = lo_d(r0);
+          sAB[2 * t + 1] = hi_d(r0);
+        }
+        if (t + NT < NCH) {
+          sAB[2 * (t + NT)] = lo_d(r1);
+          sAB[2 * (t + NT) + 1] = hi_d(r1);
+        }
+      }
       __syncthreads();
+      TL_AB(it);
       if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
         const double errv = sqrt(fmax(sAB[NOUT], 0.0));
         if (it0 + it == 0) sLoss[4] = errv;
         sLoss[5] = errv;
       }
     }
-    wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+    if (l2rows && it == 0 && w == 0) {
+      // every member has written its XCC (at its start, before its first arrival): the group's rows
+      // may go through the L2 when all of them share this workgroup's XCC (the same answer in every
+      // member: they read the same table)
+      const uint32_t xm = l < gs ? __hip_atomic_load(a.cnt + CNT_XCC0 + g + NG * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (uint32_t)sFlag[5];
+      const bool same = __ballot(xm != (uint32_t)sFlag[5]) == 0;
+      if (l == 0) sFlag[4] = same ? 1 : 0;
+    }
+    if constexpr (R6) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
+    else wt_update_basis_r5<KK>(smem, t, a.l1H, a.l2H);
     load_basis();
     TL(it, 1);
   };
@@ -5836,6 +6130,10 @@ static bool use_bfw(int x_dtype, int F, int k) {
          k * (F + k) >= 1024 && bw::lds(F).total <= (int)kMaxLds;
 }
 static PassFn bfw_fn(int F, int k) {
+#ifdef CNMF_DIAG  // CNMF_BFW_HTERMS=2: phase 1 with H in two bf16 terms (round-6 experiment, not kept)
+  if (bm::ksteps(F) == 10 && k == 16 && diag_env("CNMF_BFW_HTERMS") && atoi(diag_env("CNMF_BFW_HTERMS")) == 2)
+    return reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<10, 16, 2>);
+#endif
   return (bm::ksteps(F) == 10 && k == 16) ? reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<10, 16>)
                                           : reinterpret_cast<PassFn>(&mu_pass_bfw_kernel<0, 0>);
 }
@@ -7670,7 +7968,7 @@ static constexpr int64_t kWmuMaxBlocks = 512;  // two per CU resident (occupancy
 
 extern "C" {
 
-int cnmf_abi_version(void) { return 301; }
+int cnmf_abi_version(void) { return 302; }
 
 const char* cnmf_last_error(void) { return g_err; }
 
@@ -8042,6 +8340,16 @@ int cnmf_debug_resume_phases(unsigned long long* host_out, int reset) {  // [16]
     unsigned long long z[16] = {0};
     HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_ph), z, sizeof(z)));
   }
+  return CNMF_OK;
+}
+int cnmf_debug_levels(unsigned long long* host_out) {  // g_tl_lv, g_tl_pre, g_tl_seen, g_tl_ab (mu_iter_wt_kernel)
+  HIP_CHECK(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_tl_lv), sizeof(unsigned long long) * TL_IT * (TL_LVG + 1) * 2));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2, HIP_SYMBOL(g_tl_pre),
+                                sizeof(unsigned long long) * TL_IT * TL_WG));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2 + TL_IT * TL_WG, HIP_SYMBOL(g_tl_seen),
+                                sizeof(unsigned long long) * TL_IT * TL_WG));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2 + 2 * TL_IT * TL_WG, HIP_SYMBOL(g_tl_ab),
+                                sizeof(unsigned long long) * TL_IT * TL_WG));
   return CNMF_OK;
 }
 int cnmf_debug_xtimeline(unsigned long long* host_out) {
@@ -8524,6 +8832,12 @@ int cnmf_als_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, d
                         n_features, k, sum_to_one, smoothness, xctl, events, n_events, stream);
 }
 
+// the first reduction level through the XCD's L2 (PersistArgs::l2rows); CNMF_WT_L2ROWS in the
+// diagnostic build overrides the default
+static int wt_l2rows() {
+  const char* v = diag_env("CNMF_WT_L2ROWS");
+  return v ? (atoi(v) != 0) : 0;
+}
 static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, double* H64, double* Ht, double* HHt,
                      double* partials, double* stage, uint32_t* counter, double* AB, double l1_W, double l2_W,
                      double l1_H, double l2_H, int apply_first, int apply_last, hipStream_t s, uint64_t* xctl,
@@ -8554,6 +8868,7 @@ static int launch_wt(const WtLaunch& L, int n_iter, const void* X, void* W, doub
   pa.apply_last = apply_last;
   pa.xctl = xctl;
   pa.tolctl = tolctl;
+  pa.l2rows = L.mf ? 0 : wt_l2rows();
   void* args[] = {&pa};
   HIP_CHECK(hipLaunchKernel(L.fn, dim3((unsigned)L.G), dim3(NT), args, L.lds, s));
   return CNMF_OK;

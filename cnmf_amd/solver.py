@@ -133,10 +133,11 @@ class MUPlan:
         self.Ht = torch.zeros((self.F, KP), dtype=f64, device=dev)
         self.HHt = torch.zeros((KP, KP), dtype=f64, device=dev)
         # partial rows, stage and AB leave room for the loss column of the device tolerance test
-        # (cnmf_mu_fit_tol: rows of n_out + 1); the other launches use rows of n_out in the same memory
-        self._partials = torch.zeros(max(self.n_parts, 1) * (self.n_out + 1), dtype=f64, device=dev)
+        # (cnmf_mu_fit_tol: rows of n_out + 2 — the loss and a pad, ABI 302; the ALS form: n_out + 1);
+        # the other launches use rows of n_out in the same memory
+        self._partials = torch.zeros(max(self.n_parts, 1) * (self.n_out + 2), dtype=f64, device=dev)
         self.partials = self._partials[:max(self.n_parts, 1) * self.n_out].view(max(self.n_parts, 1), self.n_out)
-        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out + 1)), dtype=f64, device=dev)
+        self.stage = torch.zeros(int(self.lib.cnmf_stage_doubles(self.n_out + 2)), dtype=f64, device=dev)
         self.counter = torch.zeros(int(self.lib.cnmf_counter_words()), dtype=torch.int32, device=dev)
         self.err_word = int(self.lib.cnmf_counter_err_word())
         with torch.cuda.device(self.device):
@@ -159,7 +160,7 @@ class MUPlan:
         self.layout = 0  # layout of the persistent launch (include/cnmf_hip.h; 0 = default); tune() sets it
         self.shard_steps = False  # True: the multi-GPU iteration (shard step + all_reduce) at any world
         self.exchange = False  # True: multi-GPU iterations as one launch per rank (enable_exchange)
-        self._AB = torch.zeros(self.n_out + 1, dtype=f64, device=dev)
+        self._AB = torch.zeros(self.n_out + 2, dtype=f64, device=dev)
         self.AB = self._AB[:self.n_out]
         self.loss_buf = torch.zeros(1, dtype=f64, device=dev)
         self.stats = torch.zeros(2, dtype=f64, device=dev)

@@ -201,8 +201,8 @@ int cnmf_mu_iterations_multi(int n_iter, const void* X, int x_dtype, void* W, do
  * as ONE launch that also evaluates ‖X − W·H‖ of the state after g iterations (g = it0, it0 + 10,
  * ...: in the pass of iteration g + 1, which already reads x and w) and stops on the device when
  * (previous − error) / error_at_init < tol — sklearn's n_iter, W and H exactly as its loop leaves
- * them.  Buffers as cnmf_mu_iterations' except: partials rows, stage and AB hold k·(F+k) + 1
- * doubles (the loss column); tolctl = cnmf_tolctl_doubles(max_iter) doubles with, set by the
+ * them.  Buffers as cnmf_mu_iterations' except: partials rows, stage and AB hold k·(F+k) + 2
+ * doubles (the loss column and a pad: ABI 302, rows of whole 16-byte chunks); tolctl = cnmf_tolctl_doubles(max_iter) doubles with, set by the
  * caller: [CNMF_TC_TOL] tol (> 0), [CNMF_TC_IT0] it0 (global index of the launch's first
  * iteration; its errors go to slots g / 10), [CNMF_TC_CAP] error slots after CNMF_TC_ERRS,
  * [CNMF_TC_WSNAP] a device buffer of n_rows·k floats (bits of the pointer; used when W is streamed,

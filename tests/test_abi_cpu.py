@@ -37,7 +37,7 @@ def test_error_paths_return_status():
     for v in (1, 2, 3):
         assert lib.cnmf_persist_describe(1024, 81, 4, 0, v, b"\0" * 64, 64) == -1
         assert b"diagnostic" in lib.cnmf_last_error()
-    assert lib.cnmf_abi_version() == 301
+    assert lib.cnmf_abi_version() == 302
 
 
 def test_product_library_has_no_diagnostic_switches():

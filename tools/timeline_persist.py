@@ -156,6 +156,45 @@ def main():
             "slot_loads_sum": round(float(np.median(x[:, 3] - x[:, 2])) * 10 / 1e3, 2),
             "to_publish": round(float(np.median(p_ - x[:, 3])) * 10 / 1e3, 2),
             "arrival_to_start": round(float(np.median(x[:, 0] - arr[1:n - 1].max(axis=1))) * 10 / 1e3, 2)}
+    flv = getattr(lib, "cnmf_debug_levels", None)
+    if flv is not None and a.solver == "mu" and a.k in (4, 8):  # the reduction tree, level by level
+        flv.argtypes = [ctypes.c_void_p]
+        flv.restype = ctypes.c_int
+        LVG = 64
+        nlv = TL_IT * (LVG + 1) * 2
+        lb = np.zeros(nlv + 3 * TL_IT * TL_WG, dtype=np.uint64)
+        _lib.check(flv(lb.ctypes.data), "levels")
+        lv = lb[:nlv].reshape(TL_IT, LVG + 1, 2).astype(np.int64)
+        pre = lb[nlv:nlv + TL_IT * TL_WG].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
+        seen = lb[nlv + TL_IT * TL_WG:nlv + 2 * TL_IT * TL_WG].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
+        abl = lb[nlv + 2 * TL_IT * TL_WG:].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
+        ng = int(np.count_nonzero(lv[1, :LVG, 0]))
+        us = lambda v: round(float(np.median(v)) * 10 / 1e3, 2)  # noqa: E731
+        its = range(1, n - 1)
+        last_arr = np.array([arr[i].max() for i in its])
+        grp_t = np.array([lv[i, :ng, 0].max() for i in its])
+        grp_d = np.array([lv[i, :ng, 1].max() for i in its])
+        top_t = np.array([lv[i, LVG, 0] for i in its])
+        top_d = np.array([lv[i, LVG, 1] for i in its])
+        pubs = np.array([pub[i] for i in its])
+        last_wg = [int(np.argmax(arr[i])) for i in its]
+        summary["tree_us_median"] = {
+            "groups": ng,
+            "partial_row_store_median_wg": us(np.concatenate([arr[i] - pre[i] for i in its])),
+            "partial_row_store_last_arriver": us([arr[i][w] - pre[i][w] for i, w in zip(its, last_wg)]),
+            "last_arrival_to_last_group_ticket": us(grp_t - last_arr),
+            "group_combine_median": us(np.concatenate([lv[i, :ng, 1] - lv[i, :ng, 0] for i in its])),
+            "last_group_combine": us([lv[i, np.argmax(lv[i, :ng, 0]), 1] - lv[i, :ng, 0].max() for i in its]),
+            "last_group_row_to_top_ticket": us(top_t - grp_d),
+            "top_combine": us(top_d - top_t),
+            "top_done_to_flag": us(pubs - top_d),
+        }
+        nt_ = [np.nonzero(seen[i] > pub[i] - 10)[0] for i in its]  # the workgroups that polled the flag
+        summary["resume_us_median"] = {
+            "flag_to_seen": us(np.concatenate([seen[i][m] - pub[i] for i, m in zip(its, nt_)])),
+            "seen_to_ab_in_lds": us(np.concatenate([abl[i][m] - seen[i][m] for i, m in zip(its, nt_)])),
+            "ab_to_basis_ready": us(np.concatenate([res[i][m] - abl[i][m] for i, m in zip(its, nt_)])),
+        }
     if a.solver == "als":  # H-step of workgroup 0: BPP iterations and cycles per row, per call
         fh = lib.cnmf_debug_hstep
         fh.argtypes = [ctypes.c_void_p]

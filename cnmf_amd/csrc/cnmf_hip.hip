@@ -2955,6 +2955,7 @@ __device__ unsigned long long g_tl_lv[TL_IT * (TL_LVG + 1) * 2];
 __device__ unsigned long long g_tl_pre[TL_IT * TL_WG];
 __device__ unsigned long long g_tl_seen[TL_IT * TL_WG];  // flag seen (non-top workgroups)
 __device__ unsigned long long g_tl_ab[TL_IT * TL_WG];    // AB in LDS (non-top workgroups)
+__device__ unsigned long long g_tl_upd[TL_IT * TL_WG];   // basis update done (before load_basis)
 #define TL_LV(it_, g_, slot_)                                                                   \
   do {                                                                                          \
     if (t == 0 && (it_) < TL_IT) g_tl_lv[((it_) * (TL_LVG + 1) + (g_)) * 2 + (slot_)] = __builtin_amdgcn_s_memrealtime(); \
@@ -2962,6 +2963,7 @@ __device__ unsigned long long g_tl_ab[TL_IT * TL_WG];    // AB in LDS (non-top w
 #define TL_PRE(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_pre[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_SEEN(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_seen[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_AB(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_ab[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define TL_UPD(it_) do { if (t == 0 && (it_) < TL_IT && b < TL_WG) g_tl_upd[(it_) * TL_WG + b] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_X(it_, slot_) do { if (t == 0 && (it_) < TL_IT) g_tl_x[(it_) * 4 + (slot_)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define TL_START                                                                               \
   do {                                                                                         \
@@ -2983,6 +2985,7 @@ __device__ unsigned long long g_tl_ab[TL_IT * TL_WG];    // AB in LDS (non-top w
 #define TL_PRE(it_) do {} while (0)
 #define TL_SEEN(it_) do {} while (0)
 #define TL_AB(it_) do {} while (0)
+#define TL_UPD(it_) do {} while (0)
 #endif
 
 // The cross-rank all-reduce of AB (k(F+k) fp64) inside a persistent launch, run by the top
@@ -3844,8 +3847,20 @@ __device__ __forceinline__ void wt_hht(unsigned char* smem, int t) {
   static_assert(TPE * NE == NT && (TPE == 4 || TPE == 16), "threads per HHᵀ entry: a quad or a DPP row");
   const int en = t / TPE, part = t - en * TPE;
   const int j = en / KK, m = en - (en / KK) * KK;
+  // the strided products with a compile-time trip count: every LDS read of the row pair issued
+  // before the first FMA (a runtime loop waited on each iteration's reads in turn)
+  constexpr int NF = (wt::F + TPE - 1) / TPE;
+  double hj[NF], hm[NF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int f = part + TPE * i < wt::F ? part + TPE * i : wt::F - 1;
+    hj[i] = sH[j * wt::F + f];
+    hm[i] = sH[m * wt::F + f];
+  }
   double v = 0.0;
-  for (int f = part; f < wt::F; f += TPE) v = fma(sH[j * wt::F + f], sH[m * wt::F + f], v);
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+    if (part + TPE * i < wt::F) v = fma(hj[i], hm[i], v);
   v += wt::dpp64<0xB1>(v);  // quad_perm [1,0,3,2]
   v += wt::dpp64<0x4E>(v);  // quad_perm [2,3,0,1]
   if constexpr (TPE == 16) {
@@ -4597,6 +4612,7 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     }
     if constexpr (R6) wt_update_basis<KK>(smem, t, a.l1H, a.l2H);
     else wt_update_basis_r5<KK>(smem, t, a.l1H, a.l2H);
+    TL_UPD(it);
     load_basis();
     TL(it, 1);
   };
@@ -7031,7 +7047,7 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
     // the workgroup's fp64 row [A | D]: the four waves' sums in wave order (deterministic)
     {
       double* prow = a.partials + (size_t)b * NOUT;
-      for (int o = t; o < NOUT; o += NT) {
+      auto row_val = [&](int o) {
         const int isd = o >= KF ? 1 : 0;
         const int r = o - isd * KF;
         const int j = r / wt::F;
@@ -7039,8 +7055,14 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
         const int ee = f / NQ;
         const float* rr = red + ee * NACC + isd * NQ * KK + (f - NQ * ee) * KK + j;
         constexpr int WS = NL * NACC;  // wave stride
-        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
-        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+      };
+      // pairs of doubles, one 16-byte sc1 store each (round 6: the tree's hand-offs in 16-byte chunks)
+      static_assert(NOUT % 2 == 0, "[A | D] rows are whole 16-byte chunks");
+      if constexpr (MULTI) {  // (the multi-GPU form keeps the round-5 hand-offs throughout)
+        for (int o = t; o < NOUT; o += NT) __hip_atomic_store(prow + o, row_val(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (int c = t; c < NOUT / 2; c += NT) st16_sc1v(prow + 2 * c, row_val(2 * c), row_val(2 * c + 1));
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its sc1 stores landed
@@ -7054,7 +7076,9 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
     }
     __syncthreads();
     if (sFlag[0]) {  // group combiner
-      sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      // (the MULTI form keeps the 8-byte sum: at 512 registers the 16-byte batches spilled)
+      if constexpr (MULTI) sum_rows_n<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
+      else sum_rows_v<NOUT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUT, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -7063,8 +7087,12 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AD
-        sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAD, a.AD, t);
-        if (MULTI) xchg_allreduce_n<NOUT>(a.xctl, a.AD, sAD, err, it, t);  // + the other ranks' [A|D]
+        if constexpr (MULTI) {
+          sum_rows_n<NOUT>(a.groups, 0, 1, NG, sAD, a.AD, t);
+          xchg_allreduce_n<NOUT>(a.xctl, a.AD, sAD, err, it, t);  // + the other ranks' [A|D]
+        } else {
+          sum_rows_v<NOUT>(a.groups, 0, 1, NG, sAD, a.AD, t);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t == 0 && !last_it)
@@ -7117,7 +7145,24 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
         alive = false;
         return;
       }
-      for (int o = t; o < NOUT; o += NT) sAD[o] = ld_sc1(a.AD + o);
+      if constexpr (MULTI) {
+        for (int o = t; o < NOUT; o += NT) sAD[o] = ld_sc1(a.AD + o);
+      } else {  // 16-byte sc1 loads, all in flight together (round 6)
+        constexpr int NCH = NOUT / 2;
+        const int c0 = t < NCH ? t : 0, c1 = t + NT < NCH ? t + NT : 0;
+        u32x4 r0, r1;
+        ld16_sc1(r0, a.AD + 2 * c0);
+        if (NCH > NT) ld16_sc1(r1, a.AD + 2 * c1);
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(r0), "+v"(r1) : : "memory");
+        if (t < NCH) {
+          sAD[2 * t] = lo_d(r0);
+          sAD[2 * t + 1] = hi_d(r0);
+        }
+        if (t + NT < NCH) {
+          sAD[2 * (t + NT)] = lo_d(r1);
+          sAD[2 * (t + NT) + 1] = hi_d(r1);
+        }
+      }
       __syncthreads();
     }
     ww_update_basis(smem, t);
@@ -7288,6 +7333,10 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
   static_assert(!TOL || MX, "the device tolerance test is the MX kernel's");
   constexpr int KK = wa::K, NL = wa::NL, NQ = wa::NQ, V = wa::V, NOUT = wa::NOUT, NACC = wa::NACC;
   constexpr int NOUTT = NOUT + (TOL ? 1 : 0);  // partial-row width: + the loss of the checked state
+  // round 6: the reduction tree's hand-offs as 16-byte sc1 loads / stores where the rows are whole
+  // chunks (NOUTT even: not the TOL form, whose rows keep cnmf_als_fit_tol's k(F+k) + 1)
+  constexpr bool VT = NOUTT % 2 == 0;
+  static_assert(!VT || NOUTT / 2 <= NT, "one 16-byte chunk of a row per thread");
   constexpr int XBW = G4::XBW, XSTR = G4::XSTR, PFW = G4::PFW, LASTL = G4::LASTL;
   // MX: the W-step starts from the passive set of the tile's previous W (WARM, round 5), so its W is
   // loaded with X, as the TOL form's loss needs it too
@@ -7758,15 +7807,19 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       if (TOL && t == 0)
         __hip_atomic_store(prow + NOUT, (sLoss[0] + sLoss[1]) + (sLoss[2] + sLoss[3]), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      for (int o = t; o < NOUT; o += NT) {
+      auto row_val = [&](int o) {
         const int j = o / V;
         const int v = o - j * V;
         const int ee = v < wa::F ? v / NQ : j;
         const int idx = v < wa::F ? (v - NQ * ee) * KK + j : NQ * KK + (v - wa::F);
         const float* rr = red + ee * NACC + idx;
         constexpr int WS = NL * NACC;
-        const double val = ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
-        __hip_atomic_store(prow + o, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return ((double)rr[0] + (double)rr[WS]) + ((double)rr[2 * WS] + (double)rr[3 * WS]);
+      };
+      if constexpr (VT) {  // pairs of doubles, one 16-byte sc1 store each (round 6)
+        if (t < NOUT / 2) st16_sc1v(prow + 2 * t, row_val(2 * t), row_val(2 * t + 1));
+      } else {
+        for (int o = t; o < NOUT; o += NT) __hip_atomic_store(prow + o, row_val(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -7784,7 +7837,8 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     // stop there must reach every workgroup before the top applies the last H-step)
     const bool must_wait = !last_it || loss_it;
     if (sFlag[0]) {  // group combiner
-      sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
+      if constexpr (VT) sum_rows_v<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
+      else sum_rows_n<NOUTT>(a.partials, g, NG, gs, nullptr, a.groups + (size_t)g * NOUTT, t);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (t == 0) {
@@ -7793,7 +7847,12 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
       }
       __syncthreads();
       if (sFlag[1]) {  // top combiner: AB
-        sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        if constexpr (VT) {
+          sum_rows_v<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+          if (MULTI) __syncthreads();  // the exchange reads sAB in sum_rows_n's thread mapping
+        } else {
+          sum_rows_n<NOUTT>(a.groups, 0, 1, NG, sAB, a.AB, t);
+        }
         if (MULTI) xchg_allreduce_n<NOUTT>(a.xctl, a.AB, sAB, err, it, t);  // + the other ranks' AB
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -7898,12 +7957,22 @@ __global__ __launch_bounds__(NT, OCC) void als_iter_wt_kernel(AlsPersistArgs a) 
     if (!top) {
       // AB straight into the H-step's A / B arrays (TOL's loss slot into sAB)
       double* hA = reinterpret_cast<double*>(smem + wa::L_HS);
-      for (int o = t; o < NOUTT; o += NT) {
-        const double v = ld_sc1(a.AB + o);
+      auto put = [&](int o, double v) {
         const int j = o / V, c = o - j * V;
         if (o >= NOUT) sAB[o] = v;
         else if (c < wa::F) hA[j * wa::F + c] = v;
         else hA[2 * KK * wa::F + j * KK + (c - wa::F)] = v;
+      };
+      if constexpr (VT) {  // one 16-byte sc1 load per thread (round 6)
+        u32x4 r;
+        ld16_sc1(r, a.AB + 2 * (t < NOUT / 2 ? t : 0));
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(r) : : "memory");
+        if (t < NOUT / 2) {
+          put(2 * t, lo_d(r));
+          put(2 * t + 1, hi_d(r));
+        }
+      } else {
+        for (int o = t; o < NOUTT; o += NT) put(o, ld_sc1(a.AB + o));
       }
       __syncthreads();
       if (TOL && loss_it && t == 0) {  // the top went on: prev <- this check's error
@@ -8349,6 +8418,8 @@ int cnmf_debug_levels(unsigned long long* host_out) {  // g_tl_lv, g_tl_pre, g_t
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2 + TL_IT * TL_WG, HIP_SYMBOL(g_tl_seen),
                                 sizeof(unsigned long long) * TL_IT * TL_WG));
   HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2 + 2 * TL_IT * TL_WG, HIP_SYMBOL(g_tl_ab),
+                                sizeof(unsigned long long) * TL_IT * TL_WG));
+  HIP_CHECK(hipMemcpyFromSymbol(host_out + TL_IT * (TL_LVG + 1) * 2 + 3 * TL_IT * TL_WG, HIP_SYMBOL(g_tl_upd),
                                 sizeof(unsigned long long) * TL_IT * TL_WG));
   return CNMF_OK;
 }

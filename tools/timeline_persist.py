@@ -29,6 +29,9 @@ def main():
                     help="als: the persistent constrained ALS (sum_to_one 1, smoothness 0.5); wmu: the "
                          "persistent weighted MU (30 %% zero weights)")
     ap.add_argument("--layout", type=int, default=0, help="the plan's persistent layout (0 = default)")
+    ap.add_argument("--tol", type=float, default=0.0,
+                    help="> 0: the stamped launch is the device tolerance test's (cnmf_mu_fit_tol); a tol "
+                         "small enough never stops it")
     ap.add_argument("--exchange", action="store_true",
                     help="the multi-GPU launch exchanging with itself (world-1 gloo group)")
     a = ap.parse_args()
@@ -77,7 +80,10 @@ def main():
         _lib.check(fph(np.zeros(16, dtype=np.uint64).ctypes.data, 1), "resume phases")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    plan.iterate(a.iters)
+    if a.tol > 0:
+        plan.fit_device_tol(a.iters, a.tol)
+    else:
+        plan.iterate(a.iters)
     e1.record()
     torch.cuda.synchronize()
     launch_us = e0.elapsed_time(e1) * 1e3
@@ -162,12 +168,13 @@ def main():
         flv.restype = ctypes.c_int
         LVG = 64
         nlv = TL_IT * (LVG + 1) * 2
-        lb = np.zeros(nlv + 3 * TL_IT * TL_WG, dtype=np.uint64)
+        lb = np.zeros(nlv + 4 * TL_IT * TL_WG, dtype=np.uint64)
         _lib.check(flv(lb.ctypes.data), "levels")
         lv = lb[:nlv].reshape(TL_IT, LVG + 1, 2).astype(np.int64)
         pre = lb[nlv:nlv + TL_IT * TL_WG].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
         seen = lb[nlv + TL_IT * TL_WG:nlv + 2 * TL_IT * TL_WG].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
-        abl = lb[nlv + 2 * TL_IT * TL_WG:].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
+        abl = lb[nlv + 2 * TL_IT * TL_WG:nlv + 3 * TL_IT * TL_WG].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
+        upd = lb[nlv + 3 * TL_IT * TL_WG:].reshape(TL_IT, TL_WG).astype(np.int64)[:, :g]
         ng = int(np.count_nonzero(lv[1, :LVG, 0]))
         us = lambda v: round(float(np.median(v)) * 10 / 1e3, 2)  # noqa: E731
         its = range(1, n - 1)
@@ -194,6 +201,8 @@ def main():
             "flag_to_seen": us(np.concatenate([seen[i][m] - pub[i] for i, m in zip(its, nt_)])),
             "seen_to_ab_in_lds": us(np.concatenate([abl[i][m] - seen[i][m] for i, m in zip(its, nt_)])),
             "ab_to_basis_ready": us(np.concatenate([res[i][m] - abl[i][m] for i, m in zip(its, nt_)])),
+            "ab_to_update_done": us(np.concatenate([upd[i][m] - abl[i][m] for i, m in zip(its, nt_)])),
+            "update_done_to_ready": us(np.concatenate([res[i][m] - upd[i][m] for i, m in zip(its, nt_)])),
         }
     if a.solver == "als":  # H-step of workgroup 0: BPP iterations and cycles per row, per call
         fh = lib.cnmf_debug_hstep

@@ -6003,6 +6003,44 @@ __global__ __launch_bounds__(RED_NT) void reduce_kernel(const double* __restrict
                      scratch);  // fused only for KP = 4 (cnmf_reduce_update)
 }
 
+// One-level reduction for wide rows (n_out >= RW_MIN_OUT, e.g. cfg4's k(F+k) = 5056): workgroup c
+// owns 16 columns; thread (rg, c) sums rows rg, rg + 16, ... (16 independent loads in flight per
+// batch — ONE batch for <= 256 rows), then the 16 row groups in order through LDS.  No stage rows,
+// ticket or second round trip: at 256 rows × 40 KB the two-level kernel above spent its 7.7 µs on
+// its latency chain, not on the 10 MB it reads.  Fixed order: deterministic.
+constexpr int RW_MIN_OUT = 1024, RW_MAX_ROWS = 1024;
+template <int RW_COLS>
+__global__ __launch_bounds__(RED_NT) void reduce_wide_kernel(const double* __restrict__ partials,
+                                                             int64_t n_parts, int n_out,
+                                                             double* __restrict__ out) {
+  constexpr int RW_RG = RED_NT / RW_COLS;
+  __shared__ double red[RW_RG][RW_COLS];
+  const int t = threadIdx.x;
+  const int c = t % RW_COLS, rg = t / RW_COLS;
+  const int o = blockIdx.x * RW_COLS + c;
+  double s = 0.0;
+  if (o < n_out) {
+    for (int64_t b0 = rg; b0 < n_parts; b0 += (int64_t)RW_RG * 16) {
+      double x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int64_t b = b0 + (int64_t)RW_RG * u;
+        x[u] = b < n_parts ? partials[b * n_out + o] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += x[u];
+    }
+  }
+  red[rg][c] = s;
+  __syncthreads();
+  if (t < RW_COLS && o < n_out) {
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < RW_RG; ++q) v += red[q][t];
+    out[o] = v;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // HBM read probe: the achievable streaming-read ceiling on this device (16-byte loads, 8 in flight
 // per lane, grid-stride; one fp64 checksum per workgroup so nothing is dead code).
@@ -8178,6 +8216,14 @@ static int launch_reduce(const double* partials, int64_t n_parts, int n_out, dou
   if (!stage || !counter || !out || (n_parts > 0 && !partials))
     return set_err(CNMF_ERR_ARG, "null pointer argument");
   if (n_out < 1 || n_parts < 0) return set_err(CNMF_ERR_SHAPE, "invalid reduce shape");
+  if (!fuse && n_out >= RW_MIN_OUT && n_parts <= RW_MAX_ROWS) {  // wide rows: one level
+    // 16 columns per workgroup (8 and 32 measured the same at cfg4, profiles/r06/cfg4_reduce/)
+    constexpr int cols = 16;
+    hipLaunchKernelGGL(reduce_wide_kernel<cols>, dim3((unsigned)((n_out + cols - 1) / cols)), dim3(RED_NT), 0, s,
+                       partials, n_parts, n_out, out);
+    HIP_CHECK(hipGetLastError());
+    return CNMF_OK;
+  }
   const size_t lds = reduce_lds(n_out, fuse, ua.F, ua.k);
   if (lds > kMaxLds) return set_err(CNMF_ERR_UNSUPPORTED, "basis too large for the fused update");
   if (lds > 64 * 1024)

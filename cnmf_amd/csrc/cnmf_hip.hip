@@ -3557,6 +3557,33 @@ __device__ __forceinline__ float sum_over_samples(float v) {
   return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);  // + lane ^ 32
 }
 
+// Reduce-scatter of N per-lane floats over the lanes l' ≡ l (mod NL) (round 6): two permlane swap
+// levels halve the values each (permlane32_swap(x, y): the lower half-wave ends with x's pair sum,
+// the upper with y's; permlane16_swap likewise for even / odd 16-lane rows) — one swap and one add
+// per PAIR of values, where the all-reduce form spends two of each per value — and the samples
+// left inside a row are summed by DPP row rotations (ror 4 and 8 at NL = 4, ror 8 at NL = 8).
+// On return v[0 .. N/4) of every lane of row r = l / 16 hold the totals of values
+// j0 + [0, N/4) with j0 = (N/2)·(r >> 1) + (N/4)·(r & 1) (the same in the row's lanes of one class).
+template <int NL, int N>
+__device__ __forceinline__ void scatter_over_samples(float (&v)[N]) {
+  static_assert(N % 4 == 0 && (NL == 4 || NL == 8), "four quarters of the values, 4 or 8 lanes per sample");
+#pragma unroll
+  for (int j = 0; j < N / 2; ++j) {
+    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[j]), __float_as_uint(v[j + N / 2]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < N / 4; ++j) {
+    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[j]), __float_as_uint(v[j + N / 4]), false, false);
+    v[j] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+#pragma unroll
+  for (int j = 0; j < N / 4; ++j) {
+    if (NL == 4) v[j] += dppf<0x124>(v[j]);  // row_ror:4
+    v[j] += dppf<0x128>(v[j]);               // row_ror:8
+  }
+}
+
 // v summed over the 16 lanes of its row (every lane gets the row's sum)
 __device__ __forceinline__ float sum_over_row16(float v) {
   v += dppf<0x128>(v);  // row_ror:8
@@ -4359,22 +4386,31 @@ __global__ __launch_bounds__(NT, 1) void mu_iter_wt_kernel(PersistArgs a) {
     if (i + 1 != nbt) return;
 
     // ---- end of this wave's iteration: its sums over the sample lanes of each e -> LDS
+    // (reduce-scatter, round 6: value j = c·KK + 2q + comp (A), NQ·KK + 2q + comp (B); row r of the
+    // wave ends with the quarter of the values scatter_over_samples names, written by the row's
+    // lanes of sample 0, in pairs of floats)
     {
-      float* rw = red + (w * NL + e) * NACC;
+      float vv[NACC];
 #pragma unroll
       for (int c = 0; c < NQ; ++c)
 #pragma unroll
-        for (int q2 = 0; q2 < KP; q2 += 2) {
-          const float4 v = make_float4(sum_over_samples<NL>(acc[c][q2].x), sum_over_samples<NL>(acc[c][q2].y),
-                                       sum_over_samples<NL>(acc[c][q2 + 1].x), sum_over_samples<NL>(acc[c][q2 + 1].y));
-          if (l < NL) *reinterpret_cast<float4*>(rw + c * KK + 2 * q2) = v;
+        for (int q = 0; q < KP; ++q) {
+          vv[c * KK + 2 * q] = acc[c][q].x;
+          vv[c * KK + 2 * q + 1] = acc[c][q].y;
         }
 #pragma unroll
-      for (int q2 = 0; q2 < KP; q2 += 2) {
-        const float4 v = make_float4(sum_over_samples<NL>(accB[q2].x), sum_over_samples<NL>(accB[q2].y),
-                                     sum_over_samples<NL>(accB[q2 + 1].x), sum_over_samples<NL>(accB[q2 + 1].y));
-        if (l < NL) *reinterpret_cast<float4*>(rw + NQ * KK + 2 * q2) = v;
+      for (int q = 0; q < KP; ++q) {
+        vv[NQ * KK + 2 * q] = accB[q].x;
+        vv[NQ * KK + 2 * q + 1] = accB[q].y;
       }
+      scatter_over_samples<NL>(vv);
+      constexpr int NQT = NACC / 4;
+      static_assert(NQT % 2 == 0, "the quarters are written in pairs of floats");
+      const int r = l >> 4;
+      float* rw = red + (w * NL + e) * NACC + (NACC / 2) * (r >> 1) + NQT * (r & 1);
+      if ((l & 15) < NL)
+#pragma unroll
+        for (int j = 0; j < NQT; j += 2) *reinterpret_cast<float2*>(rw + j) = make_float2(vv[j], vv[j + 1]);
     }
     zero_acc();
     if (TOL) {  // the wave's loss sum (zero outside loss iterations), fixed xor tree

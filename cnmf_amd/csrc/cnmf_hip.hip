@@ -7102,6 +7102,7 @@ __global__ __launch_bounds__(NT, 1) void wmu_iter_wt_kernel(WmuPersistArgs a) {
     if (i + 1 != nbt) return;
 
     // ---- end of this wave's iteration: its sums over the sample lanes of each e -> LDS
+    // (the all-reduce form: mu_iter_wt_kernel's reduce-scatter spills this kernel past 512 registers)
     {
       float* rw = red + (w * NL + e) * NACC;
 #pragma unroll

@@ -41,3 +41,23 @@ def test_the_pd6_failure_pattern_is_flagged():
                                        "ds_write_b128 v2, a[8:11] offset:1024", "v_add_f32 v1, v2, v3"])
     assert not bad and not big
     assert kcheck.check_kernel(["s_waitcnt vmcnt(70)"])[2] == [70]
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and shutil.which(os.path.join(kcheck.LLVM, "llvm-readelf"))),
+                    reason="library or LLVM tools missing")
+def test_shipped_wave_tile_kernels_within_spill_budget():
+    """Round 6: the code object's metadata — no wave-tile kernel spills VGPRs past its family's budget
+    (0; the constrained ALS's TOL form 2, outside its streaming loop)."""
+    sp = kcheck.spills(kcheck.disassemble(LIB))
+    fam = {n: kcheck.FAMILIES.search(n).group(1) for n in sp if kcheck.FAMILIES.search(n)}
+    assert len(fam) >= 20
+    over = {n: sp[n] for n, f in fam.items() if sp[n] > kcheck.SPILL_BUDGET.get(f, 0)}
+    assert not over, over
+
+
+def test_spill_notes_parse():
+    text = ("0000 <k>:\n\tv_add_f32 v1, v2, v3\n" + kcheck.NOTES_MARK + "\n"
+            "  - .agpr_count:     0\n    .name:           _Z18wmu_iter_wt_kernelX\n    .vgpr_spill_count: 3\n"
+            "  - .agpr_count:     4\n    .name:           other\n    .vgpr_spill_count: 0\n")
+    assert kcheck.spills(text) == {"_Z18wmu_iter_wt_kernelX": 3, "other": 0}
+    assert [n for n, _ in kcheck.kernels(text)] == ["k"]

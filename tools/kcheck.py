@@ -71,13 +71,36 @@ def disassemble(lib: str, arch: str = "gfx950", llvm: str = LLVM) -> str:
              f"--targets=hipv4-amdgcn-amd-amdhsa--{arch}", f"--output={co}"])
         if not os.path.exists(co) or os.path.getsize(co) == 0:
             raise ToolError(f"{lib} holds no {arch} code object")
-        return run([f"{llvm}/llvm-objdump", "-d", "--no-show-raw-insn", co], text=True).stdout
+        dis = run([f"{llvm}/llvm-objdump", "-d", "--no-show-raw-insn", co], text=True).stdout
+        readelf = f"{llvm}/llvm-readelf"
+        notes = run([readelf, "--notes", co], text=True).stdout if os.path.exists(readelf) else ""
+        return dis + "\n" + NOTES_MARK + "\n" + notes
+
+
+NOTES_MARK = "=== kcheck: code object notes ==="
+# VGPRs spilled to scratch per kernel family (round 6, from the code object's metadata): the wave-tile
+# kernels run one or two waves per SIMD at their register ceiling, where a spill is a scratch round
+# trip inside the streaming loop.  Budgets: 0, but the constrained ALS's TOL form, whose two spilled
+# registers sit outside the loop.
+SPILL_BUDGET = {"als_iter_wt_kernel": 2}
+
+
+def spills(text: str) -> dict:
+    """{kernel symbol: VGPR spill count} from the notes part of disassemble()'s output."""
+    notes = text.split(NOTES_MARK, 1)[1] if NOTES_MARK in text else ""
+    out = {}
+    for blk in re.split(r"\n\s*- \.agpr_count", notes)[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk)
+        sp = re.search(r"\.vgpr_spill_count:\s+(\d+)", blk)
+        if name and sp:
+            out[name.group(1)] = int(sp.group(1))
+    return out
 
 
 def kernels(dis: str):
     """(name, [instruction lines]) per function of the disassembly."""
     out, name, body = [], None, []
-    for ln in dis.splitlines():
+    for ln in dis.split(NOTES_MARK, 1)[0].splitlines():
         m = re.match(r"^[0-9a-f]+ <(\S+)>:$", ln)
         if m:
             if name:
@@ -120,7 +143,8 @@ def main(lib: str, arch: str | None = None, llvm: str | None = None) -> int:
     except ToolError as e:
         print(f"kcheck: could not check {lib} ({arch}): {e}", file=sys.stderr)
         return 2
-    n_bad, n_k = 0, 0
+    n_bad, n_k, n_sp = 0, 0, 0
+    sp = spills(dis)
     for name, body in kernels(dis):
         if not FAMILIES.search(name):
             continue
@@ -131,9 +155,14 @@ def main(lib: str, arch: str | None = None, llvm: str | None = None) -> int:
             print(f"FAIL {name}: prefetch AGPRs {nreg}, {len(bad)} other touches, vmcnt > 63: {big}")
             for ins in bad[:4]:
                 print("     ", ins)
+        fam = FAMILIES.search(name).group(1)
+        if sp.get(name, 0) > SPILL_BUDGET.get(fam, 0):
+            n_sp += 1
+            print(f"FAIL {name}: {sp[name]} VGPRs spilled to scratch (budget {SPILL_BUDGET.get(fam, 0)})")
     print(f"kcheck: {n_k} wave-tile kernels checked, {n_bad} with prefetch registers touched outside "
-          f"their loads / staging / waits")
-    return 1 if n_bad or n_k == 0 else 0
+          f"their loads / staging / waits, {n_sp} over their VGPR spill budget"
+          + ("" if sp else " (no code object notes: spills not checked)"))
+    return 1 if n_bad or n_sp or n_k == 0 else 0
 
 
 if __name__ == "__main__":

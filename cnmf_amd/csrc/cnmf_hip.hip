@@ -2364,20 +2364,22 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
   // ---- basis constants: H in three bf16 terms [n][32·KS] (zero beyond F / k), HHᵀ (as bm)
   double* sHHt = reinterpret_cast<double*>(smem + L.hht);
   double* sH64 = reinterpret_cast<double*>(smem + L.total);  // PERSIST: the fp64 basis [k][F]
+  auto put_one = [&](int n, int f, double h) {
+    const uint16_t h1 = bm::bf16_rn((float)h);
+    const double r1 = h - (double)bm::bf16_f(h1);
+    const uint16_t h2 = bm::bf16_rn((float)r1);
+    const double r2 = r1 - (double)bm::bf16_f(h2);
+    const uint16_t h3 = bm::bf16_rn((float)r2);
+    uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;
+    row[0] = h1;
+    row[bm::KP * L.hrow / 2] = h2;
+    row[2 * bm::KP * L.hrow / 2] = h3;
+  };
   auto put_terms = [&](auto hval) {
     for (int e = t; e < bm::KP * 32 * KS; e += NT) {
       const int n = e / (32 * KS);
       const int f = e - n * 32 * KS;
-      const double h = (n < k && f < F) ? hval(n, f) : 0.0;
-      const uint16_t h1 = bm::bf16_rn((float)h);
-      const double r1 = h - (double)bm::bf16_f(h1);
-      const uint16_t h2 = bm::bf16_rn((float)r1);
-      const double r2 = r1 - (double)bm::bf16_f(h2);
-      const uint16_t h3 = bm::bf16_rn((float)r2);
-      uint16_t* row = reinterpret_cast<uint16_t*>(smem + L.hs + n * L.hrow) + f;
-      row[0] = h1;
-      row[bm::KP * L.hrow / 2] = h2;
-      row[2 * bm::KP * L.hrow / 2] = h3;
+      put_one(n, f, (n < k && f < F) ? hval(n, f) : 0.0);
     }
   };
   // PERSIST: the terms and HHᵀ from the fp64 basis in LDS (thread = entry (j, m) of HHᵀ: four
@@ -2419,7 +2421,27 @@ __device__ __forceinline__ void bfw_run(const BfwArgs& a) {
     __syncthreads();
     derive();
   } else {
-    put_terms([&](int n, int f) { return a.Ht[(size_t)f * bm::KP + n]; });
+    if constexpr (KSC != 0) {
+      // the pass's head (round 6): all of this thread's Hᵀ loads in flight at once (clamped addresses,
+      // no guard) — the loop above waited for each before issuing the next, one L2 round trip per
+      // entry and 20 per thread at cfg4, in every per-iteration launch
+      constexpr int NE = bm::KP * 32 * KSC, PER = (NE + NT - 1) / NT;
+      double hv[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = t + NT * u;
+        const int n = e / (32 * KSC), f = e - n * 32 * KSC;
+        hv[u] = a.Ht[(size_t)min(f, F - 1) * bm::KP + min(n, bm::KP - 1)];
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = t + NT * u;
+        const int n = e / (32 * KSC), f = e - n * 32 * KSC;
+        if (e < NE) put_one(n, f, (n < k && f < F) ? hv[u] : 0.0);
+      }
+    } else {
+      put_terms([&](int n, int f) { return a.Ht[(size_t)f * bm::KP + n]; });
+    }
     for (int e = t; e < bm::KP * bm::KP; e += NT) sHHt[e] = a.HHt[e];
   }
   zero_pads();
